@@ -1,0 +1,150 @@
+// ref_shim.cc — C entry points over the REAL reference coding path.
+//
+// TEST INFRASTRUCTURE ONLY.  Compiled by oracle/ref.mk against the reference
+// sources where they lie under /root/reference (nothing is copied into this
+// repo); the output goes to oracle/_ref/ (git-ignored).  Used only in this
+// container to generate tests/golden/ fixtures and to cross-check the C
+// restatement in oracle/oracle.c.  Never shipped, never built on the GPU box.
+//
+// It drives MemEC's own plugin exactly as its test does
+// (test/common/coding/coding.cc:149-274): Coding::instantiate -> encode(index)
+// / decode(chunks, bitmap), with Chunk buffers from TempChunkPool.
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+
+#include "common/coding/coding.hh"
+#include "common/ds/bitmask_array.hh"
+#include "common/ds/chunk_pool.hh"
+#include "common/ds/chunk_util.hh"
+
+extern "C" {
+#include "galois.h"
+#include "jerasure.h"
+#include "reed_sol.h"
+#include "cauchy.h"
+}
+
+namespace {
+struct RefHandle {
+    Coding *coding;
+    uint32_t k, m, cs;
+};
+}  // namespace
+
+extern "C" {
+
+void *ref_instantiate(int scheme, uint32_t k, uint32_t m, uint32_t chunk_size) {
+    CodingParams params;
+    CodingScheme s = scheme == 7 ? CS_CAUCHY : CS_RS;
+    params.setScheme(s);
+    params.setK(k);
+    params.setM(m);
+    ChunkUtil::init(chunk_size, k);
+    Coding *c = Coding::instantiate(s, params, chunk_size);
+    if (!c) return nullptr;
+    RefHandle *h = new RefHandle{c, k, m, chunk_size};
+    return h;
+}
+
+void ref_destroy(void *hp) {
+    RefHandle *h = (RefHandle *)hp;
+    delete h->coding;  // Coding::destroy reads an unset scheme (Appendix B #1)
+    delete h;
+}
+
+// data: k chunks of cs bytes, dense.  zero_mask bit j => pass Coding::zeros
+// for data j (the server's delta-encode form).  Writes parity `index`
+// (1-based) into out.
+void ref_encode(void *hp, const uint8_t *data, uint32_t zero_mask, uint32_t index,
+                uint8_t *out) {
+    RefHandle *h = (RefHandle *)hp;
+    TempChunkPool pool;
+    Chunk *d[64];
+    for (uint32_t j = 0; j < h->k; j++) {
+        if (zero_mask >> j & 1) {
+            d[j] = Coding::zeros;
+        } else {
+            d[j] = pool.alloc();
+            memcpy(ChunkUtil::getData(d[j]), data + (size_t)j * h->cs, h->cs);
+        }
+    }
+    Chunk *p = pool.alloc();
+    h->coding->encode(d, p, index);
+    memcpy(out, ChunkUtil::getData(p), h->cs);
+    pool.free(p);
+    for (uint32_t j = 0; j < h->k; j++)
+        if (!(zero_mask >> j & 1)) pool.free(d[j]);
+}
+
+// chunks: (k+m) chunks dense, in/out.  Missing chunks are cleared first
+// (server_peer_res_worker.cc:818-828) and rebuilt in place.
+int ref_decode(void *hp, uint8_t *chunks, uint64_t present_mask) {
+    RefHandle *h = (RefHandle *)hp;
+    uint32_t n = h->k + h->m;
+    TempChunkPool pool;
+    Chunk *c[64];
+    BitmaskArray bm(1, n);
+    for (uint32_t i = 0; i < n; i++) {
+        c[i] = pool.alloc();
+        if (present_mask >> i & 1) {
+            memcpy(ChunkUtil::getData(c[i]), chunks + (size_t)i * h->cs, h->cs);
+            bm.set(i, 0);
+        }
+    }
+    bool ok = h->coding->decode(c, &bm);
+    for (uint32_t i = 0; i < n; i++) {
+        memcpy(chunks + (size_t)i * h->cs, ChunkUtil::getData(c[i]), h->cs);
+        pool.free(c[i]);
+    }
+    return ok ? 0 : -1;
+}
+
+void ref_bitwise_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint32_t len) {
+    Coding::bitwiseXOR((char *)dst, (char *)a, (char *)b, len);
+}
+
+int ref_gf_mul(int a, int b, int w) { return galois_single_multiply(a, b, w); }
+int ref_gf_div(int a, int b, int w) { return galois_single_divide(a, b, w); }
+
+int ref_rs_matrix(int k, int m, int w, int *out) {
+    int *mat = reed_sol_vandermonde_coding_matrix(k, m, w);
+    if (!mat) return -1;
+    memcpy(out, mat, sizeof(int) * k * m);
+    free(mat);
+    return 0;
+}
+
+int ref_cauchy_matrix(int k, int m, int w, int *out) {
+    int *mat = cauchy_good_general_coding_matrix(k, m, w);
+    if (!mat) return -1;
+    memcpy(out, mat, sizeof(int) * k * m);
+    free(mat);
+    return 0;
+}
+
+int ref_cauchy_n_ones(int n, int w) { return cauchy_n_ones(n, w); }
+
+int ref_bitmatrix(int k, int m, int w, const int *matrix, int *out) {
+    int *bm = jerasure_matrix_to_bitmatrix(k, m, w, (int *)matrix);
+    if (!bm) return -1;
+    memcpy(out, bm, sizeof(int) * k * m * w * w);
+    free(bm);
+    return 0;
+}
+
+// Returns op count; ops[5*i..5*i+4].
+int ref_smart_schedule(int k, int m, int w, const int *bitmatrix, int *ops, int max_ops) {
+    int **s = jerasure_smart_bitmatrix_to_schedule(k, m, w, (int *)bitmatrix);
+    int n = 0;
+    for (; s[n][0] >= 0; n++) {
+        if (n < max_ops) memcpy(ops + 5 * n, s[n], sizeof(int) * 5);
+    }
+    jerasure_free_schedule(s);
+    return n;
+}
+
+int ref_invert_matrix(int *mat, int *inv, int n, int w) { return jerasure_invert_matrix(mat, inv, n, w); }
+int ref_invert_bitmatrix(int *mat, int *inv, int n) { return jerasure_invert_bitmatrix(mat, inv, n); }
+
+}  // extern "C"

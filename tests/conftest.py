@@ -1,0 +1,26 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+HERE = os.path.dirname(os.path.abspath(__file__))
+if HERE not in sys.path:
+    sys.path.insert(0, HERE)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libmec's HIP path)")
+    config.addinivalue_line("markers", "slow: longer CPU test")
+
+
+def pytest_collection_modifyitems(config, items):
+    pass
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import _oracle
+    return _oracle.golden()

@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures from the REAL reference coding path.
+
+Run in the build container only (needs /root/reference and
+``make -C oracle ref``).  It loads oracle/_ref/libmemec_ref.so — MemEC's own
+``Coding`` plugin over its vendored Jerasure 2.0 + gf_complete, plus ISA-L
+2.14's ec_base.c — and records inputs/outputs as data:
+
+* ``golden.json``  — matrices, bitmatrix/schedule statistics, GF samples,
+  case metadata and SHA-256 digests at full BASELINE sizes;
+* ``golden.npz``   — raw expected output bytes for the small cases.
+
+Inputs are never stored: they are regenerated from the splitmix64 stream
+(oracle.c ``orc_fill_splitmix`` == device ``mec_fill_random``) with the seed
+recorded per case.  Load the npz with ``allow_pickle=False``.
+"""
+import ctypes
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libmemec_ref.so"))
+ORC = ctypes.CDLL(os.path.join(ROOT, "oracle", "build", "liboracle.so"))
+
+CS_RS, CS_CAUCHY = 4, 7
+u8p = ctypes.POINTER(ctypes.c_uint8)
+REF.ref_instantiate.restype = ctypes.c_void_p
+REF.ref_instantiate.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+REF.ref_destroy.argtypes = [ctypes.c_void_p]
+REF.ref_encode.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint32, ctypes.c_uint32, u8p]
+REF.ref_decode.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint64]
+REF.ref_isal_gf_mul.restype = ctypes.c_uint8
+
+
+def fill(n, seed, word_offset=0):
+    buf = np.empty(n, dtype=np.uint8)
+    ORC.orc_fill_splitmix(buf.ctypes.data_as(u8p), ctypes.c_size_t(n),
+                          ctypes.c_uint64(seed), ctypes.c_uint64(word_offset))
+    return buf
+
+
+def ptr(a):
+    return a.ctypes.data_as(u8p)
+
+
+def ref_getw(scheme, k, m, cs):
+    fn = ORC.orc_rs_getw if scheme == CS_RS else ORC.orc_cauchy_getw
+    return fn(k, m, cs)
+
+
+def ref_encode_stripes(scheme, k, m, cs, n, seed):
+    """Encode n stripes with the reference plugin, parity 1..m one call each
+    (test/common/coding/coding.cc:150-152)."""
+    h = REF.ref_instantiate(scheme, k, m, cs)
+    h = ctypes.c_void_p(h)
+    data = fill(n * k * cs, seed)
+    par = np.zeros(n * m * cs, dtype=np.uint8)
+    out = np.empty(cs, dtype=np.uint8)
+    for s in range(n):
+        d = data[s * k * cs:(s + 1) * k * cs]
+        for i in range(m):
+            REF.ref_encode(h, ptr(d), ctypes.c_uint32(0), ctypes.c_uint32(i + 1), ptr(out))
+            par[(s * m + i) * cs:(s * m + i + 1) * cs] = out
+    REF.ref_destroy(h)
+    return data, par
+
+
+def ref_decode_random(scheme, k, m, cs, seed, erased):
+    """Decode a stripe of RANDOM chunks (not a codeword): pins the exact
+    linear combination the reference applies, not just uniqueness."""
+    h = ctypes.c_void_p(REF.ref_instantiate(scheme, k, m, cs))
+    chunks = fill((k + m) * cs, seed)
+    present = sum(1 << i for i in range(k + m) if i not in erased)
+    work = chunks.copy()
+    rc = REF.ref_decode(h, ptr(work), ctypes.c_uint64(present))
+    REF.ref_destroy(h)
+    out = np.concatenate([work[e * cs:(e + 1) * cs] for e in sorted(erased)]) if erased else np.zeros(0, np.uint8)
+    return rc, out
+
+
+def ref_delta(scheme, k, m, cs, seed, col, index):
+    h = ctypes.c_void_p(REF.ref_instantiate(scheme, k, m, cs))
+    data = fill(k * cs, seed)
+    out = np.empty(cs, dtype=np.uint8)
+    zero_mask = ((1 << k) - 1) & ~(1 << col)
+    REF.ref_encode(h, ptr(data), ctypes.c_uint32(zero_mask), ctypes.c_uint32(index), ptr(out))
+    REF.ref_destroy(h)
+    return out
+
+
+def main():
+    meta = {"generator": "tests/golden/make_golden.py",
+            "reference": "mtyiu/memec common/coding over lib/jerasure + lib/gf_complete; ISA-L 2.14 ec_base.c",
+            "prng": "splitmix64: word q = mix(seed + (q+1)*0x9E3779B97F4A7C15), little-endian bytes",
+            "cases": {}}
+    blobs = {}
+
+    # --- GF samples (galois_single_multiply / divide) -----------------------
+    gf = {}
+    for w in range(1, 9):
+        n = 1 << w
+        tab = [[REF.ref_gf_mul(a, b, w) for b in range(n)] for a in range(n)]
+        h = hashlib.sha256(np.array(tab, dtype=np.int32).tobytes()).hexdigest()
+        inv = [REF.ref_gf_div(1, a, w) for a in range(1, n)]
+        gf[str(w)] = {"mul_table_sha256_int32": h, "inverses": inv}
+        if w <= 4:
+            gf[str(w)]["mul_table"] = tab
+    meta["gf"] = gf
+
+    # --- matrices ------------------------------------------------------------
+    rs = {}
+    for k in range(1, 31):
+        for m in range(1, 33 - k):
+            mat = (ctypes.c_int * (k * m))()
+            if REF.ref_rs_matrix(k, m, 8, mat) == 0:
+                rs["%d,%d" % (k, m)] = list(mat)
+    meta["rs_matrices"] = rs
+
+    cau = {}
+    for w in range(2, 9):
+        for k in range(1, 33):
+            for m in range(1, 33 - k):
+                if k + m > (1 << w):
+                    continue
+                mat = (ctypes.c_int * (k * m))()
+                if REF.ref_cauchy_matrix(k, m, w, mat) != 0:
+                    continue
+                bm = (ctypes.c_int * (k * m * w * w))()
+                REF.ref_bitmatrix(k, m, w, mat, bm)
+                ops = (ctypes.c_int * (5 * (k * m * w * w + 1)))()
+                nops = REF.ref_smart_schedule(k, m, w, bm, ops, k * m * w * w + 1)
+                cau["%d,%d,%d" % (k, m, w)] = {
+                    "matrix": list(mat), "bitmatrix_ones": sum(bm),
+                    "bitmatrix_sha256_int32": hashlib.sha256(bytes(bm)).hexdigest(),
+                    "schedule_ops": nops,
+                    "schedule_sha256_int32": hashlib.sha256(bytes(ops)[:20 * nops]).hexdigest()}
+    meta["cauchy_matrices"] = cau
+    cbest = {}
+    for w in range(2, 9):
+        k = (1 << w) - 1
+        mat = (ctypes.c_int * (k * 2))()
+        REF.ref_cauchy_matrix(k, 2, w, mat)
+        cbest[str(w)] = list(mat)[k:]
+    meta["cbest"] = cbest
+
+    # --- Jerasure encode: raw small cases --------------------------------------
+    enc_cases = [
+        ("rs", 4, 2, 4096, 2), ("rs", 8, 2, 4096, 2), ("rs", 10, 4, 4096, 1),
+        ("rs", 3, 3, 64, 3), ("rs", 6, 3, 1024, 1), ("rs", 12, 4, 520, 1),
+        ("rs", 16, 16, 64, 1), ("rs", 28, 4, 72, 1), ("rs", 1, 1, 64, 1),
+        ("cauchy", 12, 4, 256, 2), ("cauchy", 4, 2, 4096, 1), ("cauchy", 8, 2, 4096, 1),
+        ("cauchy", 4, 2, 96, 2), ("cauchy", 20, 4, 320, 1), ("cauchy", 20, 4, 96, 1),
+        ("cauchy", 20, 4, 112, 1), ("cauchy", 20, 4, 64, 1), ("cauchy", 10, 4, 1024, 1),
+        ("cauchy", 6, 3, 48, 2), ("cauchy", 1, 1, 16, 1), ("cauchy", 3, 1, 24, 1),
+    ]
+    seed = 0x4D454D4543
+    for idx, (fam, k, m, cs, n) in enumerate(enc_cases):
+        scheme = CS_RS if fam == "rs" else CS_CAUCHY
+        s = seed + idx
+        _, par = ref_encode_stripes(scheme, k, m, cs, n, s)
+        name = "enc/%s/%d_%d_%d_x%d" % (fam, k, m, cs, n)
+        blobs[name] = par
+        meta["cases"][name] = {"kind": "encode", "family": fam, "k": k, "m": m, "chunk": cs,
+                               "stripes": n, "seed": s, "w": ref_getw(scheme, k, m, cs),
+                               "data_layout": "[stripe][k][chunk] from one splitmix stream",
+                               "parity_layout": "[stripe][m][chunk]"}
+
+    # --- full-size digests --------------------------------------------------------
+    big = [("rs", 10, 4, 1 << 20, 2), ("cauchy", 12, 4, 65536, 4), ("rs", 8, 2, 4096, 64),
+           ("rs", 4, 2, 4096, 64), ("cauchy", 12, 4, 65536 + 8, 1)]
+    for idx, (fam, k, m, cs, n) in enumerate(big):
+        scheme = CS_RS if fam == "rs" else CS_CAUCHY
+        s = seed + 1000 + idx
+        _, par = ref_encode_stripes(scheme, k, m, cs, n, s)
+        name = "digest/%s/%d_%d_%d_x%d" % (fam, k, m, cs, n)
+        meta["cases"][name] = {"kind": "encode_digest", "family": fam, "k": k, "m": m, "chunk": cs,
+                               "stripes": n, "seed": s, "w": ref_getw(scheme, k, m, cs),
+                               "parity_sha256": hashlib.sha256(par.tobytes()).hexdigest(),
+                               "per_chunk_sha256": [hashlib.sha256(par[i * cs:(i + 1) * cs].tobytes()).hexdigest()
+                                                    for i in range(min(n * m, 8))]}
+
+    # --- decode of random (non-codeword) stripes --------------------------------------
+    dec_cases = [
+        ("rs", 4, 2, 512, [[0], [1], [4], [5], [0, 1], [0, 4], [1, 5], [4, 5], [2, 3], [0, 5]]),
+        ("rs", 10, 4, 256, [[0, 1, 2, 3], [0, 5, 10, 13], [10, 11, 12, 13], [3], [11], [10], [2, 7], [0, 10],
+                            [1, 2, 3, 11], [9, 10, 12], [0, 1, 2, 13]]),
+        ("rs", 8, 3, 256, [[1, 2, 3], [1], [1, 2], [8, 9, 10], [0, 9], [7, 8]]),
+        ("rs", 8, 2, 4096, [[0, 1], [0], [8, 9], [3, 8]]),
+        ("cauchy", 12, 4, 256, [[0, 1, 2, 3], [0, 5, 12, 15], [12, 13, 14, 15], [3], [13], [12], [2, 7], [0, 12]]),
+        ("cauchy", 4, 2, 4096, [[0, 1], [0], [4, 5], [2, 4], [1, 5]]),
+        ("cauchy", 8, 3, 256, [[1, 2, 3], [1], [8, 9, 10], [0, 9]]),
+        ("cauchy", 20, 4, 320, [[0, 1, 2, 3], [19, 20], [21]]),
+        ("cauchy", 20, 4, 112, [[0, 1, 2, 3], [5, 22]]),
+    ]
+    for idx, (fam, k, m, cs, pats) in enumerate(dec_cases):
+        scheme = CS_RS if fam == "rs" else CS_CAUCHY
+        for p_i, pat in enumerate(pats):
+            s = seed + 2000 + 100 * idx + p_i
+            rc, out = ref_decode_random(scheme, k, m, cs, s, pat)
+            name = "dec/%s/%d_%d_%d/%s" % (fam, k, m, cs, "-".join(map(str, pat)))
+            blobs[name] = out
+            meta["cases"][name] = {"kind": "decode_random", "family": fam, "k": k, "m": m, "chunk": cs,
+                                   "seed": s, "erased": pat, "rc": rc, "w": ref_getw(scheme, k, m, cs),
+                                   "input_layout": "[k+m][chunk] random; erased chunks cleared before decode",
+                                   "output_layout": "erased chunks ascending"}
+    # too many erasures -> false
+    rc, _ = ref_decode_random(CS_RS, 4, 2, 64, 7, [0, 1, 2])
+    meta["cases"]["dec/rs/4_2_64/0-1-2"] = {"kind": "decode_fail", "family": "rs", "k": 4, "m": 2,
+                                             "chunk": 64, "erased": [0, 1, 2], "rc": rc}
+
+    # --- delta (single non-zero column, Coding::zeros elsewhere) ------------------------
+    for idx, (fam, k, m, cs, col, index) in enumerate([("rs", 8, 2, 4096, 3, 2), ("rs", 10, 4, 512, 0, 4),
+                                                      ("cauchy", 12, 4, 256, 11, 3), ("cauchy", 4, 2, 4096, 1, 1)]):
+        scheme = CS_RS if fam == "rs" else CS_CAUCHY
+        s = seed + 3000 + idx
+        out = ref_delta(scheme, k, m, cs, s, col, index)
+        name = "delta/%s/%d_%d_%d/c%d_p%d" % (fam, k, m, cs, col, index)
+        blobs[name] = out
+        meta["cases"][name] = {"kind": "delta", "family": fam, "k": k, "m": m, "chunk": cs, "seed": s,
+                               "column": col, "index": index,
+                               "data_layout": "[k][chunk] splitmix; every column but `column` is Coding::zeros"}
+
+    # --- ISA-L base family -------------------------------------------------------------
+    isal = {}
+    for (k, m) in [(4, 2), (8, 2), (10, 4), (12, 4), (6, 3)]:
+        for fam, gen in (("isal_rs", REF.ref_isal_gen_rs_matrix), ("isal_cauchy", REF.ref_isal_gen_cauchy1_matrix)):
+            a = np.zeros((k + m) * k, dtype=np.uint8)
+            gen(ptr(a), k + m, k)
+            isal["%s/%d,%d" % (fam, k, m)] = a.tolist()
+            cs, s = 512, seed + 4000 + k * 10 + m + (0 if fam == "isal_rs" else 500)
+            data = fill(k * cs, s)
+            par = np.zeros(m * cs, dtype=np.uint8)
+            coef = a[k * k:].copy()
+            src = (u8p * k)(*[ptr(data[j * cs:]) for j in range(k)])
+            dst = (u8p * m)(*[ptr(par[i * cs:]) for i in range(m)])
+            REF.ref_isal_encode(cs, k, m, ptr(coef), src, dst)
+            name = "enc/%s/%d_%d_%d_x1" % (fam, k, m, cs)
+            blobs[name] = par
+            meta["cases"][name] = {"kind": "encode", "family": fam, "k": k, "m": m, "chunk": cs, "stripes": 1,
+                                   "seed": s, "data_layout": "[k][chunk]", "parity_layout": "[m][chunk]"}
+            # update: parity ^= coef[:,col] * data[col]   (ec_encode_data_update_base)
+            col = k // 2
+            upd = par.copy()
+            dst2 = (u8p * m)(*[ptr(upd[i * cs:]) for i in range(m)])
+            delta = fill(cs, s + 1)
+            REF.ref_isal_encode_update(cs, k, m, col, ptr(coef), ptr(delta), dst2)
+            name = "upd/%s/%d_%d_%d/c%d" % (fam, k, m, cs, col)
+            blobs[name] = upd
+            meta["cases"][name] = {"kind": "update", "family": fam, "k": k, "m": m, "chunk": cs, "seed": s,
+                                   "delta_seed": s + 1, "column": col,
+                                   "semantics": "parity (enc case) ^= coef[i][col] * delta"}
+    meta["isal_matrices"] = isal
+
+    np.savez_compressed(os.path.join(HERE, "golden.npz"), **{k.replace("/", "|"): v for k, v in blobs.items()})
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(meta, f, separators=(",", ":"), sort_keys=True)
+    print("cases:", len(meta["cases"]), "blobs:", len(blobs),
+          "npz bytes:", os.path.getsize(os.path.join(HERE, "golden.npz")),
+          "json bytes:", os.path.getsize(os.path.join(HERE, "golden.json")))
+
+
+if __name__ == "__main__":
+    sys.exit(main())
