@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Device-resident stripe encode/decode throughput on MI355X.
+
+Default workload = BASELINE.json configs[1]: RS(10,4) encode, 1 MiB chunks,
+4096 stripes per GPU, inputs resident in HBM.  A "step" is one batched
+encode of the whole batch (one kernel launch).  Multi-GPU: one process per
+GPU (torchrun), stripes sharded by rank with no data-path collective
+(weak scaling: every rank encodes its own 4096-stripe batch); the barrier,
+max-over-ranks time and the final reduction use RCCL ("nccl").
+
+Prints ONE JSON line (rank 0).  value = data GiB/s (k * chunk * stripes /
+2^30 / s, the reference's MB/s convention, test/common/coding/common.hh:17-22)
+summed over all ranks.  roofline.achieved = algorithmic HBM bytes
+((k+m) * chunk per stripe for encode, (k+e) * chunk for decode) per launch /
+average launch time from HIP events on the launch stream.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident RS(k,m) encode+decode; % of HBM3E roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (family, k, m, chunk, stripes per GPU, op, erased)
+    "rs_enc": ("rs", 10, 4, 1 << 20, 4096, "encode", None),                # configs[1]
+    "rs_dec": ("rs", 10, 4, 1 << 20, 4096, "decode", [0, 1, 2, 3]),        # configs[2]
+    "rs_dec_mixed": ("rs", 10, 4, 1 << 20, 4096, "decode", [0, 5, 10, 13]),
+    "rs8_small": ("rs", 8, 2, 4096, 65536, "encode", None),                # configs[3]
+    "crs_enc": ("cauchy", 12, 4, 65536, 4096, "encode", None),             # configs[4] per GPU
+    "crs_dec": ("cauchy", 12, 4, 65536, 4096, "decode", [0, 1, 2, 3]),
+    "rs42": ("rs", 4, 2, 4096, 65536, "encode", None),
+}
+WORKLOAD_NAMES = {
+    "rs_enc": "RS(10,4) encode, 1 MiB chunks, 4096 stripes per GPU (BASELINE configs[1])",
+    "rs_dec": "RS(10,4) decode 4 erasures {0,1,2,3}, 1 MiB chunks, 4096 stripes per GPU (configs[2])",
+    "rs_dec_mixed": "RS(10,4) decode 4 erasures {0,5,10,13}, 1 MiB chunks, 4096 stripes per GPU",
+    "rs8_small": "RS(8,2) encode, 4 KiB chunks, 65536 stripes per GPU (configs[3])",
+    "crs_enc": "Cauchy-RS(12,4) encode, 64 KiB chunks, 4096 stripes per GPU (configs[4] sharded)",
+    "crs_dec": "Cauchy-RS(12,4) decode {0,1,2,3}, 64 KiB chunks, 4096 stripes per GPU",
+    "rs42": "RS(4,2) encode, 4 KiB chunks, 65536 stripes per GPU",
+}
+
+
+def cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads):
+    """Oracle restatement (same algorithm as the reference's scalar
+    Jerasure/gf_complete path) on this host, a bounded sample of the same
+    workload; its output is checked against the GPU's for those stripes."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import _oracle as O
+
+    per = k * cs
+    sample = max(threads, min(64, (768 << 20) // ((k + m) * cs)))
+    sample = (sample // threads) * threads or threads
+    data = O.fill(sample * per, seed)
+    par = np.zeros(sample * m * cs, np.uint8)
+    # 1 thread, 1 pass over `threads` stripes (single-core figure)
+    t0 = time.perf_counter()
+    O.encode_batch_mt(fam, k, m, cs, data, par, threads, 1)
+    t1 = time.perf_counter()
+    single = threads * per / (t1 - t0) / 2**30
+    passes, t_total, reps = 0, 0.0, 0
+    t0 = time.perf_counter()
+    while True:
+        O.encode_batch_mt(fam, k, m, cs, data, par, sample, threads)
+        passes += 1
+        t_total = time.perf_counter() - t0
+        if t_total * threads >= 10.0 or passes >= 64:
+            break
+    value = passes * sample * per / t_total / 2**30
+    verified = None
+    if gpu_parity_np is not None:
+        n = min(sample, gpu_parity_np.shape[0])
+        verified = bool((gpu_parity_np[:n].reshape(-1) == par[: n * m * cs]).all())
+    return {"value": round(value, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": "%d stripes x %d passes of the same workload, oracle/oracle.c orc_encode_batch_mt "
+                      "(scalar 256x256 table + 64-bit XOR, as MemEC's default build), %d threads, "
+                      "disjoint stripes per thread" % (sample, passes, threads),
+            "single_thread_value": round(single, 4), "matches_gpu": verified}
+
+
+def load_traffic(cfg_name):
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg_name)
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="rs_enc", choices=sorted(CONFIGS))
+    ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--e2e", action="store_true", help="also time the host-memory (PCIe) batch encode")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from memec_amd import Codec, fill_random
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    fam, k, m, cs, stripes, op, erased = CONFIGS[args.config]
+    if args.stripes:
+        stripes = args.stripes
+    codec = Codec(fam, k, m, cs, device=local)
+    seed = 0x4D454D4543 + rank
+
+    if op == "encode":
+        data = torch.empty(stripes, k, cs, dtype=torch.uint8, device=dev)
+        fill_random(data, seed)
+        parity = torch.empty(stripes, m, cs, dtype=torch.uint8, device=dev)
+
+        def step():
+            codec.encode(data, parity)
+        alg_bytes = (k + m) * cs * stripes
+    else:
+        stripe = torch.empty(stripes, k + m, cs, dtype=torch.uint8, device=dev)
+        d = torch.empty(stripes, k, cs, dtype=torch.uint8, device=dev)
+        fill_random(d, seed)
+        stripe[:, :k] = d
+        del d
+        codec.encode(stripe[:, :k], stripe[:, k:])
+        present = sum(1 << i for i in range(k + m) if i not in erased)
+        orig = stripe[:, erased].clone() if stripes * len(erased) * cs <= (8 << 30) else None
+        stripe[:, erased] = 0
+
+        def step():
+            codec.decode(stripe, present)
+        alg_bytes = (k + len(erased)) * cs * stripes
+    data_bytes = k * cs * stripes
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(args.steps):
+        step()
+    ev1.record()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    wall = t1 - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step
+    if world > 1:
+        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall, kern_ms = float(tt[0]), float(tt[1])
+
+    ok = None
+    if op == "decode" and orig is not None:
+        ok = bool(torch.equal(stripe[:, erased], orig))
+
+    gpu_parity_np = None
+    if rank == 0 and op == "encode" and not args.no_cpu_baseline:
+        gpu_parity_np = parity[:64].cpu().numpy()
+
+    e2e = None
+    if args.e2e and rank == 0 and op == "encode":
+        import numpy as np
+        n = min(stripes, max(8, (4 << 30) // ((k + m) * cs)))
+        hd = np.empty((n, k, cs), np.uint8)
+        hd[:] = data[:n].cpu().numpy()
+        hp = np.empty((n, m, cs), np.uint8)
+        from memec_amd import host_register, host_unregister
+        res = {}
+        for mode in ("pageable", "pinned"):
+            if mode == "pinned":
+                host_register(hd)
+                host_register(hp)
+            codec.encode_host_batch(hd, hp)
+            t2 = time.perf_counter()
+            reps = 3
+            for _ in range(reps):
+                codec.encode_host_batch(hd, hp)
+            dt = (time.perf_counter() - t2) / reps
+            res[mode] = round(n * k * cs / dt / 2**30, 3)
+            if mode == "pinned":
+                host_unregister(hd)
+                host_unregister(hp)
+        e2e = {"unit": "GiB/s data (H2D data + kernel + D2H parity)", "stripes": n, **res}
+
+    if rank == 0:
+        value = world * data_bytes * args.steps / wall / 2**30
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 stripes generated in HBM)",
+            "config": {"workload": WORKLOAD_NAMES[args.config], "family": fam, "k": k, "m": m,
+                       "chunk_bytes": cs, "stripes_per_gpu": stripes, "global_stripes": stripes * world,
+                       "op": op, "erased": erased, "parallelism": "stripe-sharded x%d" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
+                         "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4)},
+            "cpu_baseline": None,
+        }
+        if ok is not None:
+            line["decode_verified"] = ok
+        if e2e:
+            line["e2e_host_memory"] = e2e
+        if not args.no_cpu_baseline and world == 1 and op == "encode":
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            try:
+                line["cpu_baseline"] = cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads)
+            except Exception as exc:  # report, never fake
+                line["cpu_baseline"] = {"error": repr(exc)}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,182 @@
+/*
+ * mec.h — libmec: MI355X-native erasure-coding engine for MemEC's stripe
+ * encode/decode path.  Plain C ABI: opaque context, plain pointers and sizes,
+ * int status codes (never exit()).
+ *
+ * Which reference interface each entry point replaces (paths relative to the
+ * mtyiu/memec root):
+ *
+ *   mec_create / mec_destroy     Coding::instantiate / Coding::destroy
+ *                                (common/coding/coding.cc:12-54, :56-86) and
+ *                                the RSCoding / CauchyCoding constructors
+ *                                (rscoding.cc:20-43, cauchycoding.cc:20-39)
+ *   mec_encode                   Coding::encode (coding.hh:31) ->
+ *                                RSCoding::encode (rscoding.cc:51-95),
+ *                                CauchyCoding::encode (cauchycoding.cc:49-85),
+ *                                batched over stripes, device-resident
+ *   mec_decode                   Coding::decode (coding.hh:40) ->
+ *                                RSCoding::decode (rscoding.cc:97-187),
+ *                                CauchyCoding::decode (cauchycoding.cc:87-180)
+ *   mec_encode_update            the USE_ISAL delta path
+ *                                ec_encode_data_update (rscoding.cc:81-89) and
+ *                                the server's single-column delta encode
+ *                                (parity_chunk_buffer.cc:340-415)
+ *   mec_xor                      Coding::bitwiseXOR (coding.cc:88-118)
+ *   mec_encode_host /            the same calls on host-resident chunks, one
+ *   mec_decode_host /            stripe per call, as server/ issues them; the
+ *   mec_encode_update_host       C++ Coding adapter (memec_amd/csrc/coding/)
+ *                                forwards its virtual methods here
+ *   mec_encode_host_batch        host-memory (PCIe-inclusive) batched encode
+ *
+ * Memory: the device entry points take device pointers (hipMalloc / torch
+ * CUDA tensors) and a hipStream_t passed as void* (NULL = default stream);
+ * they are asynchronous on that stream.  The *_host entry points take host
+ * pointers and return when the result is in host memory.
+ *
+ * Layout of the batched device entry points ("strided"): chunk c of stripe s
+ * starts at  base + s * stripe_stride + c * chunk_stride  (bytes).  Dense
+ * [stripe][chunk][bytes] is chunk_stride = chunk_size,
+ * stripe_stride = chunks_per_stripe * chunk_size.
+ *
+ * Code families (mec_family):
+ *   MEC_RS_VANDERMONDE  Jerasure reed_sol_vandermonde_coding_matrix, GF(2^8)
+ *                       poly 0x11d, byte-wise (MemEC CS_RS, default build)
+ *   MEC_CAUCHY_GOOD     Jerasure cauchy_good_general_coding_matrix as a
+ *                       bitmatrix over w packets of chunk_size/w bytes
+ *                       (MemEC CS_CAUCHY, default build)
+ *   MEC_ISAL_RS         ISA-L gf_gen_rs_matrix, byte-wise GF(2^8)
+ *                       (MemEC CS_RS with USE_ISAL=1)
+ *   MEC_ISAL_CAUCHY     ISA-L gf_gen_cauchy1_matrix, byte-wise GF(2^8)
+ *                       (MemEC CS_CAUCHY with USE_ISAL=1)
+ */
+#ifndef MEC_H
+#define MEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MEC_ABI_VERSION 1
+#define MEC_MAX_CHUNKS 32 /* k + m <= 32: RS_N_MAX / CRS_N_MAX (rscoding.hh:5, cauchycoding.hh:5) */
+
+typedef enum {
+    MEC_OK = 0,
+    MEC_EINVAL = -1,     /* bad argument (the reference exit(-1)s here) */
+    MEC_ENOMEM = -2,     /* host or device allocation failed */
+    MEC_EHIP = -3,       /* HIP runtime error (message in mec_last_error) */
+    MEC_ETOOMANY = -4,   /* more than m chunks missing: decode returns false */
+    MEC_ESINGULAR = -5,  /* decoding matrix not invertible */
+    MEC_ENODEV = -6      /* no usable gfx950 device / kernels missing */
+} mec_status;
+
+typedef enum {
+    MEC_RS_VANDERMONDE = 0,
+    MEC_CAUCHY_GOOD = 1,
+    MEC_ISAL_RS = 2,
+    MEC_ISAL_CAUCHY = 3
+} mec_family;
+
+typedef struct mec_ctx mec_ctx;
+
+typedef struct {
+    int32_t family;
+    uint32_t k, m;
+    uint32_t w;           /* field width (8 for byte-wise families) */
+    uint32_t chunk_size;  /* bytes */
+    uint32_t packet_size; /* chunk_size / w for MEC_CAUCHY_GOOD, else chunk_size */
+    int32_t device;
+} mec_info;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+
+int mec_abi_version(void);
+/* Create a coding context on HIP device `device`.  Applies the reference's
+ * getW rules: RS w = 8 (rscoding.cc:189-220); Cauchy w = smallest w >=
+ * log2(k+m) dividing chunk_size (cauchycoding.cc:182-205), w <= 8 here.
+ * MEC_EINVAL where the reference would exit(-1). */
+int mec_create(int family, uint32_t k, uint32_t m, uint32_t chunk_size, int device,
+               mec_ctx **out);
+void mec_destroy(mec_ctx *ctx);
+/* Thread-local description of the last failure on this thread. */
+const char *mec_last_error(void);
+int mec_get_info(const mec_ctx *ctx, mec_info *out);
+/* Coding matrix: m*k int32 (Jerasure families) or (k+m)*k (ISA-L families,
+ * identity on top, as gf_gen_*_matrix produces). */
+int mec_get_matrix(const mec_ctx *ctx, int32_t *out, size_t capacity);
+/* MEC_CAUCHY_GOOD only: (m*w) x (k*w) 0/1 int32 bitmatrix
+ * (jerasure_matrix_to_bitmatrix, jerasure.c:271-297). */
+int mec_get_bitmatrix(const mec_ctx *ctx, int32_t *out, size_t capacity);
+
+/* ---- device-resident batched entry points -------------------------------- */
+
+/* Encode n_stripes stripes.  Writes parity i (0-based) for every bit i set in
+ * parity_mask (0 = all m), overwriting it (jerasure.c:603,625 overwrite too).
+ * Data and parity must not overlap. */
+int mec_encode(mec_ctx *ctx,
+               const uint8_t *data, int64_t data_stripe_stride, int64_t data_chunk_stride,
+               uint8_t *parity, int64_t parity_stripe_stride, int64_t parity_chunk_stride,
+               uint32_t n_stripes, uint32_t parity_mask, void *stream);
+
+/* Decode n_stripes stripes in place.  chunks holds all k+m chunks of every
+ * stripe (strided).  Bit i of present_mask set <=> chunk i is present
+ * (BitmaskArray::check(i), bitmask_array.cc:52-56).  Every missing chunk is
+ * rebuilt, exactly as the reference plugin computes it (same survivors, same
+ * decoding matrix).  MEC_ETOOMANY if more than m are missing; MEC_OK and no
+ * work if none is. */
+int mec_decode(mec_ctx *ctx, uint8_t *chunks, int64_t stripe_stride, int64_t chunk_stride,
+               uint32_t n_stripes, uint64_t present_mask, void *stream);
+
+/* Decode with survivors and outputs in separate buffers: reads the chunks
+ * named by present_mask from `in`, writes the missing ones to `out` (its
+ * chunk slot c for missing chunk c). */
+int mec_decode_split(mec_ctx *ctx,
+                     const uint8_t *in, int64_t in_stripe_stride, int64_t in_chunk_stride,
+                     uint8_t *out, int64_t out_stripe_stride, int64_t out_chunk_stride,
+                     uint32_t n_stripes, uint64_t present_mask, void *stream);
+
+/* Delta / update encode: parity_i ^= A[i][data_index] * delta for every bit
+ * i in parity_mask (0 = all).  Byte-wise families: one GF(2^8) scale per
+ * parity.  MEC_CAUCHY_GOOD: the column's bitmatrix block.  `delta` is one
+ * chunk per stripe. */
+int mec_encode_update(mec_ctx *ctx, uint32_t data_index,
+                      const uint8_t *delta, int64_t delta_stripe_stride,
+                      uint8_t *parity, int64_t parity_stripe_stride, int64_t parity_chunk_stride,
+                      uint32_t n_stripes, uint32_t parity_mask, void *stream);
+
+/* dst = a ^ b over len bytes (device pointers; dst may alias a or b). */
+int mec_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, void *stream);
+
+/* Benchmark / test utility: fill len device bytes with the splitmix64
+ * stream (word q = mix(seed + (q + 1) * 0x9E3779B97F4A7C15), little endian,
+ * starting at word word_offset).  Same stream as the oracle's fill. */
+int mec_fill_random(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_offset, void *stream);
+
+/* ---- host-memory entry points (one stripe; synchronous) ------------------- */
+
+/* data[j] == NULL means an all-zero chunk (the Coding::zeros sentinel,
+ * coding.cc:14-16): it is neither copied nor multiplied.  parity[i] == NULL
+ * means parity i is not wanted.  Each non-NULL parity[i] receives
+ * chunk_size bytes, overwritten. */
+int mec_encode_host(mec_ctx *ctx, const uint8_t *const *data, uint8_t *const *parity);
+/* chunks[0..k+m-1]: present chunks are read, missing ones (bit clear) are
+ * written in place. */
+int mec_decode_host(mec_ctx *ctx, uint8_t *const *chunks, uint64_t present_mask);
+/* parity[i] ^= A[i][data_index] * delta for non-NULL parity[i]. */
+int mec_encode_update_host(mec_ctx *ctx, uint32_t data_index, const uint8_t *delta,
+                           uint8_t *const *parity);
+
+/* Host-resident batch (dense [stripe][k][cs] data, [stripe][m][cs] parity),
+ * pipelined H2D -> kernel -> D2H over internal streams; returns when the
+ * parity is in host memory.  Pinned (mec_host_register) or pageable. */
+int mec_encode_host_batch(mec_ctx *ctx, const uint8_t *data, uint8_t *parity,
+                          uint32_t n_stripes, uint32_t parity_mask);
+int mec_host_register(void *ptr, size_t len);
+int mec_host_unregister(void *ptr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MEC_H */

@@ -1,0 +1,79 @@
+"""ctypes binding of libmec (include/mec.h).
+
+The shared library is built in-tree by ``make -C memec_amd`` (or
+``__graft_entry__.build()``).  There is no fallback: if libmec.so is missing
+or cannot be loaded, every entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmec.so")
+
+MEC_OK, MEC_EINVAL, MEC_ENOMEM, MEC_EHIP, MEC_ETOOMANY, MEC_ESINGULAR, MEC_ENODEV = 0, -1, -2, -3, -4, -5, -6
+FAMILIES = {"rs": 0, "cauchy": 1, "isal_rs": 2, "isal_cauchy": 3}
+
+# Exported symbols declared by include/mec.h (checked by tests/test_abi.py).
+SYMBOLS = (
+    "mec_abi_version", "mec_create", "mec_destroy", "mec_last_error", "mec_get_info",
+    "mec_get_matrix", "mec_get_bitmatrix", "mec_encode", "mec_decode", "mec_decode_split",
+    "mec_encode_update", "mec_xor", "mec_fill_random", "mec_encode_host", "mec_decode_host",
+    "mec_encode_update_host", "mec_encode_host_batch", "mec_host_register", "mec_host_unregister",
+)
+
+
+class MecError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("libmec error %d: %s" % (code, msg))
+        self.code = code
+
+
+class MecInfo(ctypes.Structure):
+    _fields_ = [("family", ctypes.c_int32), ("k", ctypes.c_uint32), ("m", ctypes.c_uint32),
+                ("w", ctypes.c_uint32), ("chunk_size", ctypes.c_uint32),
+                ("packet_size", ctypes.c_uint32), ("device", ctypes.c_int32)]
+
+
+_lib = None
+u8p = ctypes.POINTER(ctypes.c_uint8)
+vp = ctypes.c_void_p
+i64 = ctypes.c_int64
+u32 = ctypes.c_uint32
+u64 = ctypes.c_uint64
+
+
+def lib():
+    """Load libmec.so (raises if it is missing: no CPU fallback exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise MecError(MEC_ENODEV, "libmec.so not built at %s (run make -C memec_amd)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    L.mec_last_error.restype = ctypes.c_char_p
+    L.mec_create.argtypes = [ctypes.c_int, u32, u32, u32, ctypes.c_int, ctypes.POINTER(vp)]
+    L.mec_destroy.argtypes = [vp]
+    L.mec_destroy.restype = None
+    L.mec_get_info.argtypes = [vp, ctypes.POINTER(MecInfo)]
+    L.mec_get_matrix.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_size_t]
+    L.mec_get_bitmatrix.argtypes = [vp, ctypes.POINTER(ctypes.c_int32), ctypes.c_size_t]
+    L.mec_encode.argtypes = [vp, vp, i64, i64, vp, i64, i64, u32, u32, vp]
+    L.mec_decode.argtypes = [vp, vp, i64, i64, u32, u64, vp]
+    L.mec_decode_split.argtypes = [vp, vp, i64, i64, vp, i64, i64, u32, u64, vp]
+    L.mec_encode_update.argtypes = [vp, u32, vp, i64, vp, i64, i64, u32, u32, vp]
+    L.mec_xor.argtypes = [vp, vp, vp, u64, vp]
+    L.mec_fill_random.argtypes = [vp, u64, u64, u64, vp]
+    L.mec_encode_host.argtypes = [vp, ctypes.POINTER(vp), ctypes.POINTER(vp)]
+    L.mec_decode_host.argtypes = [vp, ctypes.POINTER(vp), u64]
+    L.mec_encode_update_host.argtypes = [vp, u32, vp, ctypes.POINTER(vp)]
+    L.mec_encode_host_batch.argtypes = [vp, vp, vp, u32, u32]
+    L.mec_host_register.argtypes = [vp, ctypes.c_size_t]
+    L.mec_host_unregister.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc < 0:
+        raise MecError(rc, lib().mec_last_error().decode(errors="replace"))
+    return rc

@@ -1,0 +1,153 @@
+"""Python host binding of libmec for tests, bench and Python callers.
+
+Device-resident batches are torch uint8 CUDA tensors shaped
+[stripes, chunks, chunk_size] (any stripe/chunk strides, unit byte stride);
+work is enqueued on torch's current stream.  Host entry points take numpy
+uint8 arrays.  Every call goes through the C ABI (include/mec.h) into the
+HIP kernels; there is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+vp = ctypes.c_void_p
+
+
+def _stream(stream):
+    if stream is not None:
+        return vp(stream)
+    import torch
+    return vp(torch.cuda.current_stream().cuda_stream)
+
+
+def _dev3(t, name):
+    if not t.is_cuda or t.dtype.itemsize != 1 or t.dim() != 3 or t.stride(2) != 1:
+        raise ValueError("%s must be a uint8 CUDA tensor [stripes, chunks, bytes] with unit byte stride" % name)
+    return vp(t.data_ptr()), t.stride(0), t.stride(1)
+
+
+class Codec:
+    """One coding context: family in {"rs", "cauchy", "isal_rs", "isal_cauchy"}.
+
+    device=-1 makes a host-only context (matrices only; compute raises)."""
+
+    def __init__(self, family, k, m, chunk_size, device=0):
+        self._h = vp()
+        fam = _lib.FAMILIES[family] if isinstance(family, str) else int(family)
+        check(lib().mec_create(fam, k, m, chunk_size, device, ctypes.byref(self._h)))
+        inf = _lib.MecInfo()
+        check(lib().mec_get_info(self._h, ctypes.byref(inf)))
+        self.family, self.k, self.m, self.w = family, inf.k, inf.m, inf.w
+        self.chunk_size, self.packet_size, self.device = inf.chunk_size, inf.packet_size, inf.device
+
+    def close(self):
+        if self._h:
+            lib().mec_destroy(self._h)
+            self._h = vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- matrices -----------------------------------------------------------
+    def matrix(self):
+        cap = (self.k + self.m) * self.k
+        out = (ctypes.c_int32 * cap)()
+        n = check(lib().mec_get_matrix(self._h, out, cap))
+        return list(out)[:n]
+
+    def bitmatrix(self):
+        cap = self.m * self.w * self.k * self.w
+        out = (ctypes.c_int32 * cap)()
+        n = check(lib().mec_get_bitmatrix(self._h, out, cap))
+        return list(out)[:n]
+
+    # ---- device batches -------------------------------------------------------
+    def encode(self, data, parity, parity_mask=0, stream=None):
+        d, dss, dcs = _dev3(data, "data")
+        p, pss, pcs = _dev3(parity, "parity")
+        n = data.shape[0]
+        if parity.shape[0] != n or data.shape[1] < self.k or parity.shape[1] < self.m:
+            raise ValueError("shape mismatch")
+        if data.shape[2] != self.chunk_size or parity.shape[2] != self.chunk_size:
+            raise ValueError("chunk size mismatch")
+        check(lib().mec_encode(self._h, d, dss, dcs, p, pss, pcs, n, parity_mask, _stream(stream)))
+
+    def decode(self, chunks, present_mask, stream=None):
+        c, ss, cs = _dev3(chunks, "chunks")
+        if chunks.shape[1] < self.k + self.m or chunks.shape[2] != self.chunk_size:
+            raise ValueError("shape mismatch")
+        check(lib().mec_decode(self._h, c, ss, cs, chunks.shape[0], present_mask, _stream(stream)))
+
+    def decode_split(self, src, dst, present_mask, stream=None):
+        a, ass, acs = _dev3(src, "src")
+        b, bss, bcs = _dev3(dst, "dst")
+        if src.shape[0] != dst.shape[0]:
+            raise ValueError("shape mismatch")
+        check(lib().mec_decode_split(self._h, a, ass, acs, b, bss, bcs, src.shape[0], present_mask,
+                                     _stream(stream)))
+
+    def encode_update(self, data_index, delta, parity, parity_mask=0, stream=None):
+        if not delta.is_cuda or delta.dim() != 2 or delta.stride(1) != 1:
+            raise ValueError("delta must be a uint8 CUDA tensor [stripes, bytes]")
+        p, pss, pcs = _dev3(parity, "parity")
+        check(lib().mec_encode_update(self._h, data_index, vp(delta.data_ptr()), delta.stride(0), p, pss, pcs,
+                                      parity.shape[0], parity_mask, _stream(stream)))
+
+    # ---- host, one stripe -------------------------------------------------------
+    def encode_host(self, data, want=None):
+        """data: k numpy uint8 arrays (None = all-zero chunk).  Returns the
+        wanted parities (list; None where not wanted)."""
+        cs = self.chunk_size
+        want = [True] * self.m if want is None else want
+        out = [np.empty(cs, np.uint8) if w else None for w in want]
+        dp = (vp * self.k)(*[vp(a.ctypes.data) if a is not None else vp() for a in data])
+        pp = (vp * self.m)(*[vp(a.ctypes.data) if a is not None else vp() for a in out])
+        check(lib().mec_encode_host(self._h, dp, pp))
+        return out
+
+    def decode_host(self, chunks, present_mask):
+        cp = (vp * (self.k + self.m))(*[vp(a.ctypes.data) for a in chunks])
+        check(lib().mec_decode_host(self._h, cp, present_mask))
+
+    def encode_update_host(self, data_index, delta, parity):
+        pp = (vp * self.m)(*[vp(a.ctypes.data) if a is not None else vp() for a in parity])
+        check(lib().mec_encode_update_host(self._h, data_index, vp(delta.ctypes.data), pp))
+
+    def encode_host_batch(self, data, parity, parity_mask=0):
+        """data: numpy [S, k, cs] contiguous; parity: numpy [S, m, cs] contiguous."""
+        assert data.flags.c_contiguous and parity.flags.c_contiguous
+        check(lib().mec_encode_host_batch(self._h, vp(data.ctypes.data), vp(parity.ctypes.data),
+                                          data.shape[0], parity_mask))
+
+
+def fill_random(t, seed, word_offset=0, stream=None):
+    """Fill a contiguous uint8 CUDA tensor with the splitmix64 stream."""
+    if not t.is_cuda or not t.is_contiguous():
+        raise ValueError("contiguous CUDA tensor required")
+    check(lib().mec_fill_random(vp(t.data_ptr()), t.numel() * t.element_size(), seed, word_offset,
+                                _stream(stream)))
+
+
+def xor(dst, a, b, stream=None):
+    n = dst.numel() * dst.element_size()
+    check(lib().mec_xor(vp(dst.data_ptr()), vp(a.data_ptr()), vp(b.data_ptr()), n, _stream(stream)))
+
+
+def host_register(arr):
+    check(lib().mec_host_register(vp(arr.ctypes.data), arr.nbytes))
+
+
+def host_unregister(arr):
+    check(lib().mec_host_unregister(vp(arr.ctypes.data)))

@@ -1,0 +1,83 @@
+// gpu_coding.cc — RSCoding / CauchyCoding bodies over libmec.
+#include "gpu_coding.hh"
+
+#include <stdio.h>
+#include <stdlib.h>
+
+static int adapter_device() {
+    const char *e = getenv("MEMEC_GPU_DEVICE");
+    return e ? atoi(e) : 0;
+}
+
+GpuMatrixCoding::GpuMatrixCoding(int family, const char *name, uint32_t k, uint32_t m, uint32_t chunkSize)
+    : _name(name), _family(family), _k(k), _m(m), _chunkSize(chunkSize), _ctx(0) {
+    // Parameter errors exit(-1) with a message, like rscoding.cc:26-29 and
+    // rscoding.cc:205-213 / cauchycoding.cc:193-196.
+    int rc = mec_create(family, k, m, chunkSize, adapter_device(), &_ctx);
+    if (rc != MEC_OK) {
+        fprintf(stderr, "%s: %s\n", _name, mec_last_error());
+        exit(-1);
+    }
+}
+
+GpuMatrixCoding::~GpuMatrixCoding() { mec_destroy(_ctx); }
+
+// rscoding.cc:51-95 / cauchycoding.cc:49-85: only parity `index` (1-based)
+// is written; an out-of-range index writes nothing (as idx-k == index-1
+// never matches there).  Coding::zeros columns are skipped outright — they
+// contribute nothing — which turns the server's single-column delta encodes
+// into one scale of one chunk.
+void GpuMatrixCoding::encode(Chunk **dataChunks, Chunk *parityChunk, uint32_t index, uint32_t startOff,
+                             uint32_t endOff) {
+    if (index < 1 || index > _m) return;
+    uint8_t *parity[32] = {0};
+    parity[index - 1] = (uint8_t *)ChunkUtil::getData(parityChunk);
+    int rc;
+#ifdef USE_ISAL
+    if (startOff != 0 || endOff != 0) {
+        // ec_encode_data_update over the touched columns, XORed in place.
+        rc = MEC_OK;
+        for (uint32_t i = startOff / _chunkSize; rc == MEC_OK && i <= (endOff - 1) / _chunkSize && i < _k; i++) {
+            if (dataChunks[i] == Coding::zeros) continue;
+            rc = mec_encode_update_host(_ctx, i, (const uint8_t *)ChunkUtil::getData(dataChunks[i]), parity);
+        }
+        if (rc != MEC_OK) fprintf(stderr, "%s::encode: %s\n", _name, mec_last_error());
+        return;
+    }
+#else
+    (void)startOff;
+    (void)endOff;
+#endif
+    const uint8_t *data[32];
+    for (uint32_t j = 0; j < _k; j++)
+        data[j] = dataChunks[j] == Coding::zeros ? 0 : (const uint8_t *)ChunkUtil::getData(dataChunks[j]);
+    rc = mec_encode_host(_ctx, data, parity);
+    if (rc != MEC_OK) fprintf(stderr, "%s::encode: %s\n", _name, mec_last_error());
+}
+
+// rscoding.cc:97-187 / cauchycoding.cc:87-180.
+bool GpuMatrixCoding::decode(Chunk **chunks, BitmaskArray *chunkStatus) {
+    uint32_t failed = 0;
+    uint64_t present = 0;
+    for (uint32_t i = 0; i < _k + _m; i++) {
+        if (chunkStatus->check(i))
+            present |= uint64_t(1) << i;
+        else
+            failed++;
+    }
+    if (failed > _m) {
+        fprintf(stderr, "%s: Too many failure to recover (%d>%d)!!\n", _name, failed, _m);
+        return false;
+    }
+    if (failed == 0) return true;
+    uint8_t *ptrs[32];
+    for (uint32_t i = 0; i < _k + _m; i++) ptrs[i] = (uint8_t *)ChunkUtil::getData(chunks[i]);
+    int rc = mec_decode_host(_ctx, ptrs, present);
+    if (rc != MEC_OK) {
+        // The reference ignores jerasure's return code; a device failure is
+        // reported instead of silently returning unrepaired chunks.
+        fprintf(stderr, "%s::decode: %s\n", _name, mec_last_error());
+        return false;
+    }
+    return true;
+}

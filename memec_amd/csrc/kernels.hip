@@ -1,0 +1,143 @@
+// kernels.hip — libmec's CDNA4 (gfx950) kernels.
+//
+// Every kernel is a streaming pass over HBM: each lane owns one 16-byte
+// column slice ("unit") of a stripe and touches it in every chunk it reads
+// or writes, so a wave moves 1 KiB contiguous per chunk per instruction and
+// no byte is read twice.  The arithmetic is chosen to stay under the HBM
+// time (SURVEY §7 "hard parts"):
+//
+//  * gf8_kernel — GF(2^8) matrix apply, byte-wise (Jerasure RS, ISA-L RS and
+//    Cauchy; replaces gf_w8_table_multiply_region, gf_w8.c:1033-1056 and
+//    ISA-L's gf_Nvect_dot_prod_*).  A product c*x is linear in x's bits, so
+//    a byte is split into bit fields 0-2 | 3-5 | 6-7 and each field indexes
+//    a <= 8-entry table of c*(field) with one v_perm_b32 (4 bytes per
+//    instruction).  Per (coefficient, dword): 3 v_perm + 3 v_xor.
+//  * bm_kernel  — bitmatrix packet XOR (Jerasure Cauchy-RS; replaces
+//    jerasure_do_scheduled_operations, jerasure.c:1162-1185).  Masks are
+//    kernel arguments (SGPRs); each (output packet, input packet) pair is an
+//    AND with a 0/-1 mask and an XOR.
+//  * xor_kernel — region XOR (Coding::bitwiseXOR, coding.cc:88-118).
+//  * fill_kernel — splitmix64 fill for synthetic stripes.
+#include <array>
+#include <utility>
+
+#include "gf_math.hpp"
+#include "kernels.hpp"
+#include "stream_common.hpp"
+
+namespace mec {
+namespace detail {
+template <int K, int R>
+hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream);
+template <int W, int R>
+hipError_t run_bm(const BmLaunch &L, hipStream_t stream);
+}  // namespace detail
+
+using namespace detail;
+
+Gf8Coef gf8_coef(uint8_t c) {
+    const Field &f = Field::get(8);
+    auto pack = [&](unsigned a, unsigned b, unsigned cc, unsigned d) {
+        return uint32_t(f.mul(c, a)) | uint32_t(f.mul(c, b)) << 8 | uint32_t(f.mul(c, cc)) << 16 |
+               uint32_t(f.mul(c, d)) << 24;
+    };
+    Gf8Coef r;
+    r.t0 = pack(0, 1, 2, 3);
+    r.t1 = pack(4, 5, 6, 7);
+    r.u0 = pack(0, 8, 16, 24);
+    r.u1 = pack(32, 40, 48, 56);
+    r.v = pack(0, 64, 128, 192);
+    return r;
+}
+
+namespace {
+
+using Gf8Fn = hipError_t (*)(const Gf8Launch &, hipStream_t);
+
+template <size_t... I>
+constexpr std::array<Gf8Fn, sizeof...(I)> make_gf8_table(std::index_sequence<I...>) {
+    return {{&run_gf8<int(I / kMaxRows) + 1, int(I % kMaxRows) + 1>...}};
+}
+const auto kGf8Table = make_gf8_table(std::make_index_sequence<kMaxSrc * kMaxRows>{});
+
+using BmFn = hipError_t (*)(const BmLaunch &, hipStream_t);
+
+template <size_t... I>
+constexpr std::array<BmFn, sizeof...(I)> make_bm_table(std::index_sequence<I...>) {
+    return {{&run_bm<int(I / kMaxRows) + 1, int(I % kMaxRows) + 1>...}};
+}
+const auto kBmTable = make_bm_table(std::make_index_sequence<8 * kMaxRows>{});
+
+// ---------------------------------------------------------------------------
+// XOR and fill
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void xor_kernel(uint8_t *dst, const uint8_t *a, const uint8_t *b,
+                                                       uint64_t len) {
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads * 16;
+    for (uint64_t off = (uint64_t(blockIdx.x) * kThreads + threadIdx.x) * 16; off < len; off += stride) {
+        if (off + 16 <= len) {
+            *reinterpret_cast<u32x4 *>(dst + off) =
+                *reinterpret_cast<const u32x4 *>(a + off) ^ *reinterpret_cast<const u32x4 *>(b + off);
+        } else {
+            const uint32_t n = uint32_t(len - off);
+            store_partial(dst + off, load_partial(a + off, n) ^ load_partial(b + off, n), n);
+        }
+    }
+}
+
+__device__ __forceinline__ uint64_t splitmix(uint64_t seed, uint64_t q) {
+    uint64_t z = seed + (q + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kThreads) void fill_kernel(uint8_t *dst, uint64_t len, uint64_t seed,
+                                                        uint64_t word_offset) {
+    const uint64_t stride = uint64_t(gridDim.x) * kThreads * 16;
+    for (uint64_t off = (uint64_t(blockIdx.x) * kThreads + threadIdx.x) * 16; off < len; off += stride) {
+        const uint64_t q = word_offset + off / 8;
+        const uint64_t a = splitmix(seed, q), b = splitmix(seed, q + 1);
+        const u32x4 v{uint32_t(a), uint32_t(a >> 32), uint32_t(b), uint32_t(b >> 32)};
+        if (off + 16 <= len)
+            *reinterpret_cast<u32x4 *>(dst + off) = v;
+        else
+            store_partial(dst + off, v, uint32_t(len - off));
+    }
+}
+
+uint32_t stream_blocks(uint64_t len) {
+    uint64_t b = (len + uint64_t(kThreads) * 16 - 1) / (uint64_t(kThreads) * 16);
+    return uint32_t(std::min<uint64_t>(std::max<uint64_t>(b, 1), 256 * 16));
+}
+
+}  // namespace
+
+hipError_t launch_gf8(const Gf8Launch &L, hipStream_t stream) {
+    if (L.k < 1 || L.k > kMaxSrc || L.rows < 1 || L.rows > kMaxRows) return hipErrorInvalidValue;
+    if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
+    if (L.len > (uint64_t(UINT32_MAX) - 1) * 16) return hipErrorInvalidValue;
+    return kGf8Table[size_t(L.k - 1) * kMaxRows + size_t(L.rows - 1)](L, stream);
+}
+
+hipError_t launch_bm(const BmLaunch &L, hipStream_t stream) {
+    if (L.k < 1 || L.k > kMaxSrc || L.rows < 1 || L.rows > kMaxRows || L.w < 1 || L.w > 8)
+        return hipErrorInvalidValue;
+    if (L.packet == 0 || L.n_stripes == 0) return hipSuccess;
+    return kBmTable[size_t(L.w - 1) * kMaxRows + size_t(L.rows - 1)](L, stream);
+}
+
+hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, hipStream_t stream) {
+    if (len == 0) return hipSuccess;
+    hipLaunchKernelGGL(xor_kernel, dim3(stream_blocks(len)), dim3(kThreads), 0, stream, dst, a, b, len);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_offset, hipStream_t stream) {
+    if (len == 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_kernel, dim3(stream_blocks(len)), dim3(kThreads), 0, stream, dst, len, seed,
+                       word_offset);
+    return hipGetLastError();
+}
+
+}  // namespace mec

@@ -1,0 +1,570 @@
+// mec.cpp — libmec C ABI (include/mec.h): coding contexts, plan caching,
+// kernel dispatch and host-memory staging.
+#include "mec.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gf_math.hpp"
+#include "kernels.hpp"
+
+using mec::Field;
+using mec::Mat;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    return fail(MEC_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// Staging resources for the host-memory entry points (one per concurrent
+// caller; server workers share one context, worker.cc:128-137).
+struct Lane {
+    hipStream_t stream = nullptr;
+    uint8_t *dev = nullptr;  // (k + m) chunk slots
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct mec_ctx {
+    int family;
+    uint32_t k, m, w, cs, packet;
+    int device;
+    Mat A;  // m x k (Jerasure) or (k+m) x k (ISA-L)
+    std::mutex plan_mu;
+    std::unordered_map<uint64_t, std::shared_ptr<mec::LinearPlan>> plans;
+    std::mutex lane_mu;
+    std::vector<Lane *> lanes_free;
+    std::vector<Lane *> lanes_all;
+    // pipelined host batch
+    std::mutex batch_mu;
+    hipStream_t bstream[2] = {nullptr, nullptr};
+    uint8_t *bdev[2] = {nullptr, nullptr};
+    size_t bbytes = 0;
+
+    bool byte_wise() const { return family != MEC_CAUCHY_GOOD; }
+    mec::Scheme scheme() const {
+        return family == MEC_RS_VANDERMONDE ? mec::Scheme::kJerasureRS
+               : family == MEC_CAUCHY_GOOD  ? mec::Scheme::kJerasureCauchy
+                                            : mec::Scheme::kIsal;
+    }
+    // coefficient of parity row i (0..m-1), data column j
+    uint8_t coef(uint32_t i, uint32_t j) const {
+        return byte_wise() && family != MEC_RS_VANDERMONDE ? A[size_t(k + i) * k + j] : A[size_t(i) * k + j];
+    }
+};
+
+namespace {
+
+bool has_device(const mec_ctx *c) { return c->device >= 0; }
+
+// outputs (^)= coef (n_dst x n_src over GF(2^w)) * sources, every stripe.
+int apply(mec_ctx *c, const uint8_t *src, int64_t sss, const std::vector<int64_t> &src_off, uint8_t *dst,
+          int64_t dss, const std::vector<int64_t> &dst_off, const Mat &coef, uint32_t n_stripes, bool accumulate,
+          hipStream_t stream) {
+    const size_t ns = src_off.size(), nd = dst_off.size();
+    if (nd == 0 || n_stripes == 0) return MEC_OK;
+    if (ns == 0) {  // all-zero input: outputs are zero (or unchanged when accumulating)
+        if (accumulate) return MEC_OK;
+        for (uint32_t s = 0; s < n_stripes; ++s)
+            for (size_t r = 0; r < nd; ++r)
+                HIP_TRY(hipMemsetAsync(dst + int64_t(s) * dss + dst_off[r], 0, c->cs, stream));
+        return MEC_OK;
+    }
+    for (size_t r0 = 0; r0 < nd; r0 += mec::kMaxRows) {
+        const int rows = int(std::min<size_t>(mec::kMaxRows, nd - r0));
+        if (c->byte_wise()) {
+            mec::Gf8Launch L{};
+            L.src = src;
+            L.dst = dst;
+            L.src_stripe_stride = sss;
+            L.dst_stripe_stride = dss;
+            L.k = int(ns);
+            L.rows = rows;
+            L.len = c->cs;
+            L.n_stripes = n_stripes;
+            L.accumulate = accumulate;
+            for (size_t j = 0; j < ns; ++j) L.src_off[j] = src_off[j];
+            for (int i = 0; i < rows; ++i) {
+                L.dst_off[i] = dst_off[r0 + i];
+                for (size_t j = 0; j < ns; ++j) L.coef[i][j] = mec::gf8_coef(coef[(r0 + i) * ns + j]);
+            }
+            HIP_TRY(mec::launch_gf8(L, stream));
+        } else {
+            const Field &f = Field::get(int(c->w));
+            mec::BmLaunch L{};
+            L.src = src;
+            L.dst = dst;
+            L.src_stripe_stride = sss;
+            L.dst_stripe_stride = dss;
+            L.k = int(ns);
+            L.rows = rows;
+            L.w = int(c->w);
+            L.packet = c->packet;
+            L.n_stripes = n_stripes;
+            L.accumulate = accumulate;
+            for (size_t j = 0; j < ns; ++j) L.src_off[j] = src_off[j];
+            for (int i = 0; i < rows; ++i) {
+                L.dst_off[i] = dst_off[r0 + i];
+                for (size_t j = 0; j < ns; ++j) {
+                    // block (i, j) of the bitmatrix: row l, column x = bit l of coef * 2^x
+                    unsigned e = coef[(r0 + i) * ns + j];
+                    uint8_t cols[8];
+                    for (uint32_t x = 0; x < c->w; ++x) {
+                        cols[x] = uint8_t(e);
+                        e = f.mul(e, 2 % f.size());
+                    }
+                    for (uint32_t l = 0; l < c->w; ++l) {
+                        uint8_t mb = 0;
+                        for (uint32_t x = 0; x < c->w; ++x) mb |= uint8_t((cols[x] >> l & 1) << x);
+                        L.mask[j][i * c->w + l] = mb;
+                    }
+                }
+            }
+            HIP_TRY(mec::launch_bm(L, stream));
+        }
+    }
+    return MEC_OK;
+}
+
+int get_plan(mec_ctx *c, uint64_t present, std::shared_ptr<mec::LinearPlan> &out) {
+    const uint64_t full = (uint64_t(1) << (c->k + c->m)) - 1;
+    present &= full;
+    {
+        std::lock_guard<std::mutex> g(c->plan_mu);
+        auto it = c->plans.find(present);
+        if (it != c->plans.end()) {
+            out = it->second;
+            return MEC_OK;
+        }
+    }
+    auto plan = std::make_shared<mec::LinearPlan>();
+    std::string err;
+    int rc = mec::plan_decode(c->scheme(), c->A, int(c->k), int(c->m), int(c->w), present, *plan, err);
+    if (rc != MEC_OK) return fail(rc, "decode: %s", err.c_str());
+    std::lock_guard<std::mutex> g(c->plan_mu);
+    c->plans.emplace(present, plan);
+    out = plan;
+    return MEC_OK;
+}
+
+Mat encode_rows(const mec_ctx *c, const std::vector<uint32_t> &rows, const std::vector<uint32_t> &cols) {
+    Mat m(rows.size() * cols.size());
+    for (size_t r = 0; r < rows.size(); ++r)
+        for (size_t j = 0; j < cols.size(); ++j) m[r * cols.size() + j] = c->coef(rows[r], cols[j]);
+    return m;
+}
+
+std::vector<uint32_t> mask_rows(const mec_ctx *c, uint32_t parity_mask) {
+    std::vector<uint32_t> rows;
+    if (parity_mask == 0) parity_mask = (c->m >= 32) ? 0xffffffffu : ((1u << c->m) - 1);
+    for (uint32_t i = 0; i < c->m; ++i)
+        if (parity_mask >> i & 1) rows.push_back(i);
+    return rows;
+}
+
+Lane *lane_acquire(mec_ctx *c, int &rc) {
+    {
+        std::lock_guard<std::mutex> g(c->lane_mu);
+        if (!c->lanes_free.empty()) {
+            Lane *l = c->lanes_free.back();
+            c->lanes_free.pop_back();
+            return l;
+        }
+    }
+    Lane *l = new Lane;
+    l->bytes = size_t(c->k + c->m) * c->cs;
+    hipError_t e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&l->dev, l->bytes);
+    if (e != hipSuccess) {
+        rc = hip_fail(e, "staging lane");
+        if (l->stream) (void)hipStreamDestroy(l->stream);
+        delete l;
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(c->lane_mu);
+    c->lanes_all.push_back(l);
+    return l;
+}
+
+void lane_release(mec_ctx *c, Lane *l) {
+    std::lock_guard<std::mutex> g(c->lane_mu);
+    c->lanes_free.push_back(l);
+}
+
+struct LaneHold {
+    mec_ctx *c;
+    Lane *l;
+    ~LaneHold() {
+        if (l) lane_release(c, l);
+    }
+};
+
+#define CHECK_CTX(c)                                                        \
+    do {                                                                    \
+        if (!(c)) return fail(MEC_EINVAL, "null context");                  \
+        if (!has_device(c)) return fail(MEC_ENODEV, "context has no device"); \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int mec_abi_version(void) { return MEC_ABI_VERSION; }
+
+const char *mec_last_error(void) { return g_err.c_str(); }
+
+int mec_create(int family, uint32_t k, uint32_t m, uint32_t chunk_size, int device, mec_ctx **out) {
+    if (!out) return fail(MEC_EINVAL, "out is null");
+    *out = nullptr;
+    if (family < MEC_RS_VANDERMONDE || family > MEC_ISAL_CAUCHY) return fail(MEC_EINVAL, "unknown family %d", family);
+    if (k < 1 || m < 1 || k + m > MEC_MAX_CHUNKS)
+        return fail(MEC_EINVAL, "Only support N up to %u for RS coding (k=%u, m=%u)", MEC_MAX_CHUNKS, k, m);
+    if (chunk_size == 0) return fail(MEC_EINVAL, "chunk_size is 0");
+    std::unique_ptr<mec_ctx> c(new mec_ctx);
+    c->family = family;
+    c->k = k;
+    c->m = m;
+    c->cs = chunk_size;
+    c->device = device;
+    switch (family) {
+        case MEC_RS_VANDERMONDE: {
+            int w = mec::rs_getw(k, m, chunk_size);
+            if (w != 8)
+                return fail(MEC_EINVAL, "chunkSize is not a multiple of %d bytes is of supported", 8);
+            c->w = 8;
+            if (!mec::jerasure_rs_matrix(int(k), int(m), c->A))
+                return fail(MEC_EINVAL, "No coding matrix can be generated with k=%u, m=%u, w=8", k, m);
+            break;
+        }
+        case MEC_CAUCHY_GOOD: {
+            int w = mec::cauchy_getw(k, m, chunk_size);
+            if (w < 0) return fail(MEC_EINVAL, "Cannot find a suitable w for k=%u,m=%u,chunkSize=%u", k, m, chunk_size);
+            if (w > 8) return fail(MEC_EINVAL, "Cauchy w=%d > 8 is not supported", w);
+            c->w = uint32_t(w);
+            if (!mec::jerasure_cauchy_matrix(int(k), int(m), w, c->A))
+                return fail(MEC_EINVAL, "No coding matrix can be generated with k=%u, m=%u, w=%d", k, m, w);
+            break;
+        }
+        case MEC_ISAL_RS:
+            c->w = 8;
+            c->A = mec::isal_rs_matrix(int(k), int(m));
+            break;
+        case MEC_ISAL_CAUCHY:
+            c->w = 8;
+            c->A = mec::isal_cauchy_matrix(int(k), int(m));
+            break;
+    }
+    c->packet = family == MEC_CAUCHY_GOOD ? chunk_size / c->w : chunk_size;
+    if (device >= 0) {
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess || device >= n)
+            return fail(MEC_ENODEV, "HIP device %d not available (%s)", device,
+                        e == hipSuccess ? "count" : hipGetErrorString(e));
+        hipDeviceProp_t prop;
+        e = hipGetDeviceProperties(&prop, device);
+        if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+            return fail(MEC_ENODEV, "device %d is %s; libmec is built for gfx950 only", device, prop.gcnArchName);
+    }
+    *out = c.release();
+    return MEC_OK;
+}
+
+void mec_destroy(mec_ctx *c) {
+    if (!c) return;
+    if (has_device(c)) {
+        DeviceGuard g(c->device);
+        for (Lane *l : c->lanes_all) {
+            (void)hipStreamSynchronize(l->stream);
+            (void)hipFree(l->dev);
+            (void)hipStreamDestroy(l->stream);
+            delete l;
+        }
+        for (int i = 0; i < 2; ++i) {
+            if (c->bstream[i]) {
+                (void)hipStreamSynchronize(c->bstream[i]);
+                (void)hipStreamDestroy(c->bstream[i]);
+            }
+            if (c->bdev[i]) (void)hipFree(c->bdev[i]);
+        }
+    }
+    delete c;
+}
+
+int mec_get_info(const mec_ctx *c, mec_info *out) {
+    if (!c || !out) return fail(MEC_EINVAL, "null argument");
+    out->family = c->family;
+    out->k = c->k;
+    out->m = c->m;
+    out->w = c->w;
+    out->chunk_size = c->cs;
+    out->packet_size = c->packet;
+    out->device = c->device;
+    return MEC_OK;
+}
+
+int mec_get_matrix(const mec_ctx *c, int32_t *out, size_t capacity) {
+    if (!c || !out) return fail(MEC_EINVAL, "null argument");
+    if (capacity < c->A.size()) return fail(MEC_EINVAL, "capacity %zu < %zu", capacity, c->A.size());
+    for (size_t i = 0; i < c->A.size(); ++i) out[i] = c->A[i];
+    return int(c->A.size());
+}
+
+int mec_get_bitmatrix(const mec_ctx *c, int32_t *out, size_t capacity) {
+    if (!c || !out) return fail(MEC_EINVAL, "null argument");
+    if (c->family != MEC_CAUCHY_GOOD) return fail(MEC_EINVAL, "bitmatrix exists for MEC_CAUCHY_GOOD only");
+    const uint32_t w = c->w, cols = c->k * w;
+    const size_t n = size_t(c->m) * w * cols;
+    if (capacity < n) return fail(MEC_EINVAL, "capacity %zu < %zu", capacity, n);
+    const Field &f = Field::get(int(w));
+    for (uint32_t i = 0; i < c->m; ++i)
+        for (uint32_t j = 0; j < c->k; ++j) {
+            unsigned e = c->A[size_t(i) * c->k + j];
+            for (uint32_t x = 0; x < w; ++x) {
+                for (uint32_t l = 0; l < w; ++l) out[size_t(i * w + l) * cols + j * w + x] = (e >> l) & 1;
+                e = f.mul(e, 2 % f.size());
+            }
+        }
+    return int(n);
+}
+
+int mec_encode(mec_ctx *c, const uint8_t *data, int64_t dss_, int64_t dcs, uint8_t *parity, int64_t pss, int64_t pcs,
+               uint32_t n_stripes, uint32_t parity_mask, void *stream) {
+    CHECK_CTX(c);
+    if (!data || !parity) return fail(MEC_EINVAL, "null buffer");
+    DeviceGuard dg(c->device);
+    std::vector<uint32_t> rows = mask_rows(c, parity_mask), cols(c->k);
+    for (uint32_t j = 0; j < c->k; ++j) cols[j] = j;
+    std::vector<int64_t> so(c->k), dof(rows.size());
+    for (uint32_t j = 0; j < c->k; ++j) so[j] = int64_t(j) * dcs;
+    for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(rows[r]) * pcs;
+    return apply(c, data, dss_, so, parity, pss, dof, encode_rows(c, rows, cols), n_stripes, false,
+                 hipStream_t(stream));
+}
+
+int mec_decode_split(mec_ctx *c, const uint8_t *in, int64_t iss, int64_t ics, uint8_t *out, int64_t oss, int64_t ocs,
+                     uint32_t n_stripes, uint64_t present_mask, void *stream) {
+    CHECK_CTX(c);
+    if (!in || !out) return fail(MEC_EINVAL, "null buffer");
+    std::shared_ptr<mec::LinearPlan> plan;
+    int rc = get_plan(c, present_mask, plan);
+    if (rc != MEC_OK) return rc;
+    if (plan->dst.empty()) return MEC_OK;
+    DeviceGuard dg(c->device);
+    std::vector<int64_t> so(plan->src.size()), dof(plan->dst.size());
+    for (size_t t = 0; t < so.size(); ++t) so[t] = int64_t(plan->src[t]) * ics;
+    for (size_t r = 0; r < dof.size(); ++r) dof[r] = int64_t(plan->dst[r]) * ocs;
+    return apply(c, in, iss, so, out, oss, dof, plan->coef, n_stripes, false, hipStream_t(stream));
+}
+
+int mec_decode(mec_ctx *c, uint8_t *chunks, int64_t ss, int64_t cs, uint32_t n_stripes, uint64_t present_mask,
+               void *stream) {
+    return mec_decode_split(c, chunks, ss, cs, chunks, ss, cs, n_stripes, present_mask, stream);
+}
+
+int mec_encode_update(mec_ctx *c, uint32_t data_index, const uint8_t *delta, int64_t delta_ss, uint8_t *parity,
+                      int64_t pss, int64_t pcs, uint32_t n_stripes, uint32_t parity_mask, void *stream) {
+    CHECK_CTX(c);
+    if (!delta || !parity) return fail(MEC_EINVAL, "null buffer");
+    if (data_index >= c->k) return fail(MEC_EINVAL, "data_index %u >= k %u", data_index, c->k);
+    DeviceGuard dg(c->device);
+    std::vector<uint32_t> rows = mask_rows(c, parity_mask), cols{data_index};
+    std::vector<int64_t> so{0}, dof(rows.size());
+    for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(rows[r]) * pcs;
+    return apply(c, delta, delta_ss, so, parity, pss, dof, encode_rows(c, rows, cols), n_stripes, true,
+                 hipStream_t(stream));
+}
+
+int mec_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, void *stream) {
+    if (!dst || !a || !b) return fail(MEC_EINVAL, "null buffer");
+    HIP_TRY(mec::launch_xor(dst, a, b, len, hipStream_t(stream)));
+    return MEC_OK;
+}
+
+int mec_fill_random(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_offset, void *stream) {
+    if (!dst) return fail(MEC_EINVAL, "null buffer");
+    HIP_TRY(mec::launch_fill(dst, len, seed, word_offset, hipStream_t(stream)));
+    return MEC_OK;
+}
+
+// ---- host-memory, one stripe ------------------------------------------------
+
+int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *parity) {
+    CHECK_CTX(c);
+    if (!data || !parity) return fail(MEC_EINVAL, "null pointer array");
+    DeviceGuard dg(c->device);
+    int rc = MEC_OK;
+    LaneHold h{c, lane_acquire(c, rc)};
+    if (!h.l) return rc;
+    const size_t cs = c->cs;
+    std::vector<uint32_t> rows, cols;
+    for (uint32_t i = 0; i < c->m; ++i)
+        if (parity[i]) rows.push_back(i);
+    if (rows.empty()) return MEC_OK;
+    for (uint32_t j = 0; j < c->k; ++j)
+        if (data[j]) cols.push_back(j);
+    std::vector<int64_t> so(cols.size()), dof(rows.size());
+    for (size_t t = 0; t < cols.size(); ++t) {
+        so[t] = int64_t(cols[t]) * int64_t(cs);
+        HIP_TRY(hipMemcpyAsync(h.l->dev + so[t], data[cols[t]], cs, hipMemcpyHostToDevice, h.l->stream));
+    }
+    for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(c->k + rows[r]) * int64_t(cs);
+    rc = apply(c, h.l->dev, 0, so, h.l->dev, 0, dof, encode_rows(c, rows, cols), 1, false, h.l->stream);
+    if (rc != MEC_OK) return rc;
+    for (size_t r = 0; r < rows.size(); ++r)
+        HIP_TRY(hipMemcpyAsync(parity[rows[r]], h.l->dev + dof[r], cs, hipMemcpyDeviceToHost, h.l->stream));
+    HIP_TRY(hipStreamSynchronize(h.l->stream));
+    return MEC_OK;
+}
+
+int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
+    CHECK_CTX(c);
+    if (!chunks) return fail(MEC_EINVAL, "null pointer array");
+    std::shared_ptr<mec::LinearPlan> plan;
+    int rc = get_plan(c, present_mask, plan);
+    if (rc != MEC_OK) return rc;
+    if (plan->dst.empty()) return MEC_OK;
+    DeviceGuard dg(c->device);
+    LaneHold h{c, lane_acquire(c, rc)};
+    if (!h.l) return rc;
+    const size_t cs = c->cs;
+    std::vector<int64_t> so(plan->src.size()), dof(plan->dst.size());
+    for (size_t t = 0; t < so.size(); ++t) {
+        so[t] = int64_t(plan->src[t]) * int64_t(cs);
+        HIP_TRY(hipMemcpyAsync(h.l->dev + so[t], chunks[plan->src[t]], cs, hipMemcpyHostToDevice, h.l->stream));
+    }
+    for (size_t r = 0; r < dof.size(); ++r) dof[r] = int64_t(plan->dst[r]) * int64_t(cs);
+    rc = apply(c, h.l->dev, 0, so, h.l->dev, 0, dof, plan->coef, 1, false, h.l->stream);
+    if (rc != MEC_OK) return rc;
+    for (size_t r = 0; r < dof.size(); ++r)
+        HIP_TRY(hipMemcpyAsync(chunks[plan->dst[r]], h.l->dev + dof[r], cs, hipMemcpyDeviceToHost, h.l->stream));
+    HIP_TRY(hipStreamSynchronize(h.l->stream));
+    return MEC_OK;
+}
+
+int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta, uint8_t *const *parity) {
+    CHECK_CTX(c);
+    if (!delta || !parity) return fail(MEC_EINVAL, "null pointer");
+    if (data_index >= c->k) return fail(MEC_EINVAL, "data_index %u >= k %u", data_index, c->k);
+    DeviceGuard dg(c->device);
+    int rc = MEC_OK;
+    LaneHold h{c, lane_acquire(c, rc)};
+    if (!h.l) return rc;
+    const size_t cs = c->cs;
+    std::vector<uint32_t> rows, cols{data_index};
+    for (uint32_t i = 0; i < c->m; ++i)
+        if (parity[i]) rows.push_back(i);
+    if (rows.empty()) return MEC_OK;
+    std::vector<int64_t> so{0}, dof(rows.size());
+    HIP_TRY(hipMemcpyAsync(h.l->dev, delta, cs, hipMemcpyHostToDevice, h.l->stream));
+    for (size_t r = 0; r < rows.size(); ++r) {
+        dof[r] = int64_t(1 + r) * int64_t(cs);
+        HIP_TRY(hipMemcpyAsync(h.l->dev + dof[r], parity[rows[r]], cs, hipMemcpyHostToDevice, h.l->stream));
+    }
+    rc = apply(c, h.l->dev, 0, so, h.l->dev, 0, dof, encode_rows(c, rows, cols), 1, true, h.l->stream);
+    if (rc != MEC_OK) return rc;
+    for (size_t r = 0; r < rows.size(); ++r)
+        HIP_TRY(hipMemcpyAsync(parity[rows[r]], h.l->dev + dof[r], cs, hipMemcpyDeviceToHost, h.l->stream));
+    HIP_TRY(hipStreamSynchronize(h.l->stream));
+    return MEC_OK;
+}
+
+int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint32_t n_stripes,
+                          uint32_t parity_mask) {
+    CHECK_CTX(c);
+    if (!data || !parity) return fail(MEC_EINVAL, "null buffer");
+    DeviceGuard dg(c->device);
+    std::lock_guard<std::mutex> bg(c->batch_mu);
+    const size_t cs = c->cs, dbytes = size_t(c->k) * cs, pbytes = size_t(c->m) * cs;
+    const size_t per = dbytes + pbytes;
+    const uint32_t sub = uint32_t(std::max<size_t>(1, std::min<size_t>(n_stripes, (size_t(256) << 20) / per)));
+    const size_t need = size_t(sub) * per;
+    if (c->bbytes < need) {
+        for (int i = 0; i < 2; ++i) {
+            if (c->bdev[i]) (void)hipFree(c->bdev[i]);
+            c->bdev[i] = nullptr;
+        }
+        c->bbytes = 0;
+        for (int i = 0; i < 2; ++i) HIP_TRY(hipMalloc(&c->bdev[i], need));
+        c->bbytes = need;
+    }
+    for (int i = 0; i < 2; ++i)
+        if (!c->bstream[i]) HIP_TRY(hipStreamCreateWithFlags(&c->bstream[i], hipStreamNonBlocking));
+    std::vector<uint32_t> rows = mask_rows(c, parity_mask), cols(c->k);
+    for (uint32_t j = 0; j < c->k; ++j) cols[j] = j;
+    const Mat coef = encode_rows(c, rows, cols);
+    std::vector<int64_t> so(c->k), dof(rows.size());
+    for (uint32_t j = 0; j < c->k; ++j) so[j] = int64_t(j) * int64_t(cs);
+    for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(rows[r]) * int64_t(cs);
+    int b = 0;
+    for (uint32_t s0 = 0; s0 < n_stripes; s0 += sub, b ^= 1) {
+        const uint32_t ns = std::min(sub, n_stripes - s0);
+        uint8_t *dd = c->bdev[b], *dp = c->bdev[b] + size_t(sub) * dbytes;
+        HIP_TRY(hipMemcpyAsync(dd, data + size_t(s0) * dbytes, size_t(ns) * dbytes, hipMemcpyHostToDevice,
+                               c->bstream[b]));
+        int rc = apply(c, dd, int64_t(dbytes), so, dp, int64_t(pbytes), dof, coef, ns, false, c->bstream[b]);
+        if (rc != MEC_OK) return rc;
+        HIP_TRY(hipMemcpyAsync(parity + size_t(s0) * pbytes, dp, size_t(ns) * pbytes, hipMemcpyDeviceToHost,
+                               c->bstream[b]));
+    }
+    HIP_TRY(hipStreamSynchronize(c->bstream[0]));
+    HIP_TRY(hipStreamSynchronize(c->bstream[1]));
+    return MEC_OK;
+}
+
+int mec_host_register(void *ptr, size_t len) {
+    HIP_TRY(hipHostRegister(ptr, len, hipHostRegisterDefault));
+    return MEC_OK;
+}
+
+int mec_host_unregister(void *ptr) {
+    HIP_TRY(hipHostUnregister(ptr));
+    return MEC_OK;
+}
+
+}  // extern "C"

@@ -122,7 +122,7 @@ def main():
     meta["rs_matrices"] = rs
 
     cau = {}
-    for w in range(2, 9):
+    for w in range(1, 9):
         for k in range(1, 33):
             for m in range(1, 33 - k):
                 if k + m > (1 << w):

@@ -1,0 +1,142 @@
+"""CPU checks of the C ABI: libmec.so loads, exports every symbol declared in
+include/mec.h, and its host-side math (matrices, getW rules, error codes)
+matches the reference fixtures.  No compute call is made (no GPU here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from memec_amd import Codec, MecError, _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_symbols():
+    src = open(os.path.join(ROOT, "include", "mec.h")).read()
+    return sorted(set(re.findall(r"\b(mec_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_exports_every_declared_symbol():
+    L = _lib.lib()
+    declared = _declared_symbols()
+    assert len(declared) >= 19
+    for name in declared:
+        assert hasattr(L, name), name
+    assert set(declared) == set(_lib.SYMBOLS)
+    assert L.mec_abi_version() == 1
+
+
+def test_coding_adapter_library_links():
+    so = os.path.join(ROOT, "memec_amd", "libmemec_coding.so")
+    assert os.path.exists(so)
+    L = ctypes.CDLL(so)
+    for sym in ("_ZN6Coding11instantiateE12CodingSchemeR12CodingParamsj", "_ZN6Coding10bitwiseXOREPcS0_S0_j"):
+        assert hasattr(L, sym), sym
+
+
+def test_rs_matrices_match_reference(golden):
+    meta, _ = golden
+    for key in ["4,2", "8,2", "10,4", "12,4", "6,3", "1,1", "16,16", "30,2", "2,30"]:
+        k, m = map(int, key.split(","))
+        with Codec("rs", k, m, 4096, device=-1) as c:
+            assert c.matrix() == meta["rs_matrices"][key], key
+            assert c.w == 8 and c.packet_size == 4096
+
+
+def test_all_rs_matrices(golden):
+    meta, _ = golden
+    for key, mat in meta["rs_matrices"].items():
+        k, m = map(int, key.split(","))
+        with Codec("rs", k, m, 64, device=-1) as c:
+            assert c.matrix() == mat, key
+
+
+def test_cauchy_matrices_and_w(golden):
+    meta, _ = golden
+    for (k, m, cs) in [(12, 4, 65536), (4, 2, 4096), (8, 2, 4096), (4, 2, 96), (20, 4, 320), (20, 4, 96),
+                       (20, 4, 112), (20, 4, 64), (10, 4, 1024), (6, 3, 48), (3, 1, 24), (1, 1, 16)]:
+        w = O.cauchy_getw(k, m, cs)
+        with Codec("cauchy", k, m, cs, device=-1) as c:
+            assert c.w == w, (k, m, cs)
+            assert c.packet_size == cs // w
+            assert c.matrix() == meta["cauchy_matrices"]["%d,%d,%d" % (k, m, w)]["matrix"], (k, m, cs)
+            bm = c.bitmatrix()
+            assert sum(bm) == meta["cauchy_matrices"]["%d,%d,%d" % (k, m, w)]["bitmatrix_ones"]
+            assert bm == O.bitmatrix(k, m, w, c.matrix())
+
+
+def test_every_cauchy_matrix(golden):
+    meta, _ = golden
+    for key, rec in meta["cauchy_matrices"].items():
+        k, m, w = map(int, key.split(","))
+        # pick the smallest chunk size for which getW lands on this w
+        cs = None
+        for cand in range(w, 8 * 64 + 1, w):
+            if O.cauchy_getw(k, m, cand) == w:
+                cs = cand
+                break
+        if cs is None:
+            continue
+        with Codec("cauchy", k, m, cs, device=-1) as c:
+            assert c.matrix() == rec["matrix"], key
+
+
+def test_isal_matrices(golden):
+    meta, _ = golden
+    for key, mat in meta["isal_matrices"].items():
+        fam, km = key.split("/")
+        k, m = map(int, km.split(","))
+        with Codec(fam, k, m, 512, device=-1) as c:
+            assert c.matrix() == mat, key
+
+
+def test_reference_parameter_errors():
+    # rscoding.cc:26-29: k + m > 32 -> exit(-1); here MEC_EINVAL
+    with pytest.raises(MecError) as e:
+        Codec("rs", 30, 3, 4096, device=-1)
+    assert e.value.code == _lib.MEC_EINVAL
+    # rscoding.cc:210-213: chunkSize % w
+    with pytest.raises(MecError):
+        Codec("rs", 4, 2, 4100, device=-1)
+    # cauchy w > 8 unsupported here (reference sizes are multiples of 8, w <= 8)
+    with pytest.raises(MecError):
+        Codec("cauchy", 20, 4, 9 * 11 * 13, device=-1)
+    with pytest.raises(MecError):
+        Codec("nope" if False else 9, 4, 2, 4096, device=-1)
+
+
+def test_host_only_context_refuses_compute():
+    with Codec("rs", 4, 2, 4096, device=-1) as c:
+        with pytest.raises(MecError) as e:
+            c.encode_host([np.zeros(4096, np.uint8)] * 4)
+        assert e.value.code == _lib.MEC_ENODEV
+
+
+def test_gf8_perm_decomposition_emulated():
+    """The device multiplies by splitting each byte into bit fields 0-2, 3-5,
+    6-7 and looking each up with v_perm_b32.  Emulate v_perm_b32 (select byte
+    s of {S0:S1}, S1 = bytes 0-3) and check every (c, x) product."""
+    def perm(s0, s1, sel):
+        b = [(s1 >> (8 * i)) & 0xFF for i in range(4)] + [(s0 >> (8 * i)) & 0xFF for i in range(4)]
+        return sum(b[(sel >> (8 * i)) & 0xFF] << (8 * i) for i in range(4))
+
+    L = O.lib()
+    mul = np.array([[L.orc_gf_mul(a, b, 8) for b in range(256)] for a in range(256)], np.uint32)
+
+    def pack(c, vals):
+        return int(sum(int(mul[c][v]) << (8 * i) for i, v in enumerate(vals)))
+
+    xs = np.arange(256, dtype=np.uint32).reshape(64, 4)
+    words = (xs[:, 0] | xs[:, 1] << 8 | xs[:, 2] << 16 | xs[:, 3] << 24).tolist()
+    for c in range(256):
+        t0, t1 = pack(c, [0, 1, 2, 3]), pack(c, [4, 5, 6, 7])
+        u0, u1 = pack(c, [0, 8, 16, 24]), pack(c, [32, 40, 48, 56])
+        v = pack(c, [0, 64, 128, 192])
+        for wi, x in enumerate(words):
+            s0, s1, s2 = x & 0x07070707, (x >> 3) & 0x07070707, (x >> 6) & 0x03030303
+            got = perm(t1, t0, s0) ^ perm(u1, u0, s1) ^ perm(v, v, s2)
+            want = sum(int(mul[c][(x >> (8 * i)) & 0xFF]) << (8 * i) for i in range(4))
+            assert got == want, (c, x)

@@ -1,0 +1,54 @@
+#!/usr/bin/env bash
+# tools/gpu_session.sh STEP... — run GPU steps on the MI355X box, each under
+# its own time limit, stopping at the first fault/abort/timeout.
+#   tests   pytest -m gpu          smoke   __graft_entry__.smoke()
+#   bench   bench.py (default)     prof    rocprofv3 --kernel-trace --stats of bench
+#   benchall  bench.py for every config (no cpu baseline)
+#   pmc     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench
+set -u
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p "$OUT"
+TAG=${TAG:-r01}
+
+run() {  # name seconds cmd...
+    local name=$1 secs=$2
+    shift 2
+    echo "=== $name: $*" | tee -a "$OUT/session.log"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc" | tee -a "$OUT/session.log"
+    tail -n 25 "$OUT/$name.log"
+    case $rc in
+        0|1|5) return 0 ;;   # pass / test failures / no tests: not a GPU fault
+        *) echo "stopping: $name rc=$rc"; exit $rc ;;
+    esac
+}
+
+for step in "$@"; do
+    case $step in
+        tests) run pytest_gpu 1100 python -m pytest tests -m gpu -x -q ;;
+        smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) run bench 400 python bench.py ;;
+        benchall)
+            for c in rs_enc rs_dec rs_dec_mixed rs8_small crs_enc crs_dec rs42; do
+                run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --steps 10
+            done ;;
+        e2e) run bench_e2e 400 python bench.py --e2e --no-cpu-baseline --steps 5 ;;
+        prof)
+            for c in ${PROF_CONFIGS:-rs_enc}; do
+                run "prof_$c" 400 rocprofv3 --kernel-trace --stats --output-format csv \
+                    -d "$OUT/prof_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 10 --warmup 2
+            done ;;
+        pmc)
+            for c in ${PROF_CONFIGS:-rs_enc}; do
+                run "pmc_fetch_$c" 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+                    -d "$OUT/pmc_fetch_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 5 --warmup 1
+                run "pmc_write_$c" 400 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+                    -d "$OUT/pmc_write_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 5 --warmup 1
+            done ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "session done"
