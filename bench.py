@@ -142,7 +142,7 @@ def main():
         del d
         codec.encode(stripe[:, :k], stripe[:, k:])
         present = sum(1 << i for i in range(k + m) if i not in erased)
-        orig = stripe[:, erased].clone() if stripes * len(erased) * cs <= (8 << 30) else None
+        orig = stripe[:, erased].clone() if stripes * len(erased) * cs <= (24 << 30) else None
         stripe[:, erased] = 0
 
         def step():

@@ -1,12 +1,19 @@
 // gf8_kernel.hpp — GF(2^8) byte-wise matrix apply (Jerasure RS, ISA-L RS /
 // Cauchy).  Instantiated per row count in gf8_r{1..4}.hip.
 //
-// A product c*x is linear in the bits of x, so each byte is split into bit
-// fields 0-2 | 3-5 | 6-7 and every field indexes a <= 8-entry table of
+// Arithmetic: c*x is linear in the bits of x, so every byte is split into
+// bit fields 0-2 | 3-5 | 6-7 and each field indexes a <= 8-entry table of
 // c*(field << shift) with one v_perm_b32, four bytes per instruction:
-// 3 v_perm + 3 v_xor per (coefficient, dword).  Replaces the scalar
-// multtable[s][c] byte loop (gf_w8.c:1047-1050) and ISA-L's PSHUFB nibble
-// kernels (gf_vect_dot_prod_sse.asm:215-230).
+// 3 v_perm + 3 v_xor per (coefficient, dword).  Coefficient 1 is a plain
+// XOR and coefficient 0 is skipped (uniform branches on kernel-argument
+// masks).  Replaces the scalar multtable[s][c] byte loop
+// (gf_w8.c:1047-1050) and ISA-L's PSHUFB nibble kernels
+// (gf_vect_dot_prod_sse.asm:215-230).
+//
+// Memory: each lane owns one 16-byte column slice of one stripe: K
+// non-temporal dwordx4 loads (one per source chunk, a wave reads 1 KiB
+// contiguous per chunk), R non-temporal dwordx4 stores.  The permute tables
+// live in LDS (R*K*32 bytes) and are read by broadcast right before use.
 #pragma once
 
 #include "stream_common.hpp"
@@ -14,28 +21,55 @@
 namespace mec {
 namespace detail {
 
-// ---------------------------------------------------------------------------
-// GF(2^8) byte-wise matrix apply
-// ---------------------------------------------------------------------------
 template <int K, int R>
 struct Gf8Params {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
-    uint64_t len;
-    uint32_t units, tiles, upt, accumulate;
+    uint32_t units, tiles, accumulate, pad;
+    uint32_t ones[4], zeros[4];  // bit i*K+j: coefficient (i, j) is 1 / 0
     int64_t src_off[K];
     int64_t dst_off[R];
     Gf8Coef coef[R][K];
 };
 
-__device__ __forceinline__ uint32_t gf8_mul(const Gf8Coef &c, uint32_t s0, uint32_t s1, uint32_t s2) {
-    return __builtin_amdgcn_perm(c.t1, c.t0, s0) ^ __builtin_amdgcn_perm(c.u1, c.u0, s1) ^
-           __builtin_amdgcn_perm(c.v, c.v, s2);
+__device__ __forceinline__ uint32_t gf8_mul(const Gf8Coef &c, uint32_t x) {
+    return __builtin_amdgcn_perm(c.t1, c.t0, x & 0x07070707u) ^
+           __builtin_amdgcn_perm(c.u1, c.u0, (x >> 3) & 0x07070707u) ^
+           __builtin_amdgcn_perm(c.v, c.v, (x >> 6) & 0x03030303u);
 }
 
 template <int K, int R>
-__device__ __forceinline__ void gf8_combine(const Gf8Params<K, R> &p, const u32x4 (&d)[K], u32x4 (&acc)[R]) {
+__global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) {
+    __shared__ uint32_t tab[R * K * 8];
+    for (int t = threadIdx.x; t < R * K; t += kThreads) {
+        const Gf8Coef c = p.coef[t / K][t % K];
+        tab[t * 8 + 0] = c.t0;
+        tab[t * 8 + 1] = c.t1;
+        tab[t * 8 + 2] = c.u0;
+        tab[t * 8 + 3] = c.u1;
+        tab[t * 8 + 4] = c.v;
+    }
+    __syncthreads();
+    const uint32_t stripe = blockIdx.x / p.tiles;
+    const uint32_t u = (blockIdx.x - stripe * p.tiles) * kThreads + threadIdx.x;
+    if (u >= p.units) return;
+    const uint64_t off = uint64_t(u) * 16;
+    const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
+    uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
+
+    u32x4 d[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) d[j] = ld_nt<u32x4>(sb + p.src_off[j]);
+    u32x4 acc[R];
+    if (p.accumulate) {
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[i] = *reinterpret_cast<const u32x4 *>(db + p.dst_off[i]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[i] = u32x4{0, 0, 0, 0};
+    }
+    const uint32_t *tb = tab + opaque_zero();
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const u32x4 x = d[j];
@@ -44,76 +78,77 @@ __device__ __forceinline__ void gf8_combine(const Gf8Params<K, R> &p, const u32x
         const u32x4 s2 = (x >> 6) & 0x03030303u;
 #pragma unroll
         for (int i = 0; i < R; ++i) {
-            const Gf8Coef &c = p.coef[i][j];
-            acc[i].x ^= gf8_mul(c, s0.x, s1.x, s2.x);
-            acc[i].y ^= gf8_mul(c, s0.y, s1.y, s2.y);
-            acc[i].z ^= gf8_mul(c, s0.z, s1.z, s2.z);
-            acc[i].w ^= gf8_mul(c, s0.w, s1.w, s2.w);
+            constexpr int kBits = 32;
+            const int b = i * K + j;
+            if ((p.zeros[b / kBits] >> (b % kBits)) & 1u) continue;
+            if ((p.ones[b / kBits] >> (b % kBits)) & 1u) {
+                acc[i] ^= x;
+                continue;
+            }
+            const u32x4 t = *reinterpret_cast<const u32x4 *>(tb + b * 8);
+            const uint32_t v = tb[b * 8 + 4];
+            acc[i].x ^= __builtin_amdgcn_perm(t.y, t.x, s0.x) ^ __builtin_amdgcn_perm(t.w, t.z, s1.x) ^
+                        __builtin_amdgcn_perm(v, v, s2.x);
+            acc[i].y ^= __builtin_amdgcn_perm(t.y, t.x, s0.y) ^ __builtin_amdgcn_perm(t.w, t.z, s1.y) ^
+                        __builtin_amdgcn_perm(v, v, s2.y);
+            acc[i].z ^= __builtin_amdgcn_perm(t.y, t.x, s0.z) ^ __builtin_amdgcn_perm(t.w, t.z, s1.z) ^
+                        __builtin_amdgcn_perm(v, v, s2.z);
+            acc[i].w ^= __builtin_amdgcn_perm(t.y, t.x, s0.w) ^ __builtin_amdgcn_perm(t.w, t.z, s1.w) ^
+                        __builtin_amdgcn_perm(v, v, s2.w);
         }
     }
+#pragma unroll
+    for (int i = 0; i < R; ++i) st_nt<u32x4>(db + p.dst_off[i], acc[i]);
 }
 
-template <int K, int R>
-__global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) {
-    const uint32_t stripe = blockIdx.x / p.tiles;
-    const uint32_t tile = blockIdx.x - stripe * p.tiles;
-    const uint8_t *sb = p.src + int64_t(stripe) * p.sss;
-    uint8_t *db = p.dst + int64_t(stripe) * p.dss;
-    const uint32_t ubase = tile * p.upt * kThreads + threadIdx.x;
-    for (uint32_t r = 0; r < p.upt; ++r) {
-        const uint32_t u = ubase + r * kThreads;
-        if (u >= p.units) return;
-        const uint64_t off = uint64_t(u) * 16;
-        u32x4 d[K], acc[R];
-        if (off + 16 <= p.len) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) d[j] = *reinterpret_cast<const u32x4 *>(sb + p.src_off[j] + off);
-#pragma unroll
-            for (int i = 0; i < R; ++i)
-                acc[i] = p.accumulate ? *reinterpret_cast<const u32x4 *>(db + p.dst_off[i] + off) : u32x4{0, 0, 0, 0};
-            gf8_combine(p, d, acc);
-#pragma unroll
-            for (int i = 0; i < R; ++i) *reinterpret_cast<u32x4 *>(db + p.dst_off[i] + off) = acc[i];
-        } else {
-            const uint32_t n = uint32_t(p.len - off);
-#pragma unroll
-            for (int j = 0; j < K; ++j) d[j] = load_partial(sb + p.src_off[j] + off, n);
-#pragma unroll
-            for (int i = 0; i < R; ++i)
-                acc[i] = p.accumulate ? load_partial(db + p.dst_off[i] + off, n) : u32x4{0, 0, 0, 0};
-            gf8_combine(p, d, acc);
-#pragma unroll
-            for (int i = 0; i < R; ++i) store_partial(db + p.dst_off[i] + off, acc[i], n);
-        }
-    }
-}
+// The < 16-byte remainder of each region (chunk sizes that are not a
+// multiple of 16): one thread per stripe, any K and row count.
+struct Gf8TailParams {
+    const uint8_t *src;
+    uint8_t *dst;
+    int64_t sss, dss;
+    uint64_t off;
+    uint32_t n, k, rows, n_stripes, accumulate, pad;
+    int64_t src_off[kMaxSrc];
+    int64_t dst_off[kMaxRows];
+    Gf8Coef coef[kMaxRows][kMaxSrc];
+};
+
+hipError_t launch_gf8_tail(const Gf8Launch &L, uint64_t off, hipStream_t stream);
 
 template <int K, int R>
 hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     Gf8Params<K, R> p;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
-    p.len = L.len;
-    const Geometry g = geometry((L.len + 15) / 16);
+    const Geometry g = geometry(L.len / 16);
     p.units = g.units;
     p.tiles = g.tiles;
-    p.upt = g.upt;
     p.accumulate = L.accumulate ? 1u : 0u;
+    p.pad = 0;
+    for (int w = 0; w < 4; ++w) p.ones[w] = p.zeros[w] = 0;
     for (int j = 0; j < K; ++j) p.src_off[j] = L.src_off[j];
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int i = 0; i < R; ++i)
-        for (int j = 0; j < K; ++j) p.coef[i][j] = L.coef[i][j];
-    for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
-        const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-        p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-        p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-        hipLaunchKernelGGL((gf8_kernel<K, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-        hipError_t e = hipGetLastError();
-        if (e != hipSuccess) return e;
+        for (int j = 0; j < K; ++j) {
+            p.coef[i][j] = L.coef[i][j];
+            const int b = i * K + j;
+            if (L.coef[i][j].t0 == 0x03020100u) p.ones[b / 32] |= 1u << (b % 32);
+            if (L.coef[i][j].t1 == 0) p.zeros[b / 32] |= 1u << (b % 32);
+        }
+    if (g.units > 0) {
+        for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
+            const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
+            p.src = L.src + int64_t(s0) * L.src_stripe_stride;
+            p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+            hipLaunchKernelGGL((gf8_kernel<K, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
     }
+    if (L.len % 16) return launch_gf8_tail(L, uint64_t(g.units) * 16, stream);
     return hipSuccess;
 }
-
 
 #define MEC_GF8_INSTANTIATE_K(R) \
     template hipError_t run_gf8<1, R>(const Gf8Launch &, hipStream_t); \

@@ -23,6 +23,8 @@
 
 #include "gf_math.hpp"
 #include "kernels.hpp"
+#include "bm_kernel.hpp"
+#include "gf8_kernel.hpp"
 #include "stream_common.hpp"
 
 namespace mec {
@@ -31,6 +33,101 @@ template <int K, int R>
 hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream);
 template <int W, int R>
 hipError_t run_bm(const BmLaunch &L, hipStream_t stream);
+
+// ---------------------------------------------------------------------------
+// Tails: the < 16-byte (gf8) / < unit (bitmatrix) remainder of each region,
+// one thread per stripe.  Only launched for sizes that are not multiples of
+// the vector unit.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void gf8_tail_kernel(const Gf8TailParams p) {
+    const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
+    if (s >= p.n_stripes) return;
+    const uint8_t *sb = p.src + int64_t(s) * p.sss + p.off;
+    uint8_t *db = p.dst + int64_t(s) * p.dss + p.off;
+    for (uint32_t i = 0; i < p.rows; ++i) {
+        u32x4 acc = p.accumulate ? load_partial(db + p.dst_off[i], p.n) : u32x4{0, 0, 0, 0};
+        for (uint32_t j = 0; j < p.k; ++j) {
+            const u32x4 x = load_partial(sb + p.src_off[j], p.n);
+            const Gf8Coef c = p.coef[i][j];
+            acc ^= u32x4{gf8_mul(c, x.x), gf8_mul(c, x.y), gf8_mul(c, x.z), gf8_mul(c, x.w)};
+        }
+        store_partial(db + p.dst_off[i], acc, p.n);
+    }
+}
+
+hipError_t launch_gf8_tail(const Gf8Launch &L, uint64_t off, hipStream_t stream) {
+    Gf8TailParams p;
+    p.src = L.src;
+    p.dst = L.dst;
+    p.sss = L.src_stripe_stride;
+    p.dss = L.dst_stripe_stride;
+    p.off = off;
+    p.n = uint32_t(L.len - off);
+    p.k = uint32_t(L.k);
+    p.rows = uint32_t(L.rows);
+    p.n_stripes = L.n_stripes;
+    p.accumulate = L.accumulate ? 1u : 0u;
+    p.pad = 0;
+    for (int j = 0; j < kMaxSrc; ++j) p.src_off[j] = L.src_off[j];
+    for (int i = 0; i < kMaxRows; ++i) {
+        p.dst_off[i] = L.dst_off[i];
+        for (int j = 0; j < kMaxSrc; ++j) p.coef[i][j] = L.coef[i][j];
+    }
+    hipLaunchKernelGGL(gf8_tail_kernel, dim3((L.n_stripes + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, p);
+    return hipGetLastError();
+}
+
+struct BmTailParams {
+    const uint8_t *src;
+    uint8_t *dst;
+    int64_t sss, dss;
+    uint64_t packet, off;
+    uint32_t n, k, rows, w, n_stripes, accumulate;
+    int64_t src_off[kMaxSrc];
+    int64_t dst_off[kMaxRows];
+    uint8_t mask[kMaxSrc][kMaxBmRows];
+};
+
+__global__ __launch_bounds__(kThreads) void bm_tail_kernel(const BmTailParams p) {
+    const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
+    if (s >= p.n_stripes) return;
+    const uint8_t *sb = p.src + int64_t(s) * p.sss + p.off;
+    uint8_t *db = p.dst + int64_t(s) * p.dss + p.off;
+    for (uint32_t i = 0; i < p.rows; ++i)
+        for (uint32_t l = 0; l < p.w; ++l) {
+            uint8_t *q = db + p.dst_off[i] + uint64_t(l) * p.packet;
+            u32x4 acc = p.accumulate ? load_partial(q, p.n) : u32x4{0, 0, 0, 0};
+            for (uint32_t j = 0; j < p.k; ++j) {
+                const uint32_t mb = p.mask[j][i * p.w + l];
+                for (uint32_t x = 0; x < p.w; ++x)
+                    if ((mb >> x) & 1u) acc ^= load_partial(sb + p.src_off[j] + uint64_t(x) * p.packet, p.n);
+            }
+            store_partial(q, acc, p.n);
+        }
+}
+
+hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream) {
+    BmTailParams p;
+    p.src = L.src;
+    p.dst = L.dst;
+    p.sss = L.src_stripe_stride;
+    p.dss = L.dst_stripe_stride;
+    p.packet = L.packet;
+    p.off = off;
+    p.n = uint32_t(L.packet - off);
+    p.k = uint32_t(L.k);
+    p.rows = uint32_t(L.rows);
+    p.w = uint32_t(L.w);
+    p.n_stripes = L.n_stripes;
+    p.accumulate = L.accumulate ? 1u : 0u;
+    for (int j = 0; j < kMaxSrc; ++j) p.src_off[j] = L.src_off[j];
+    for (int i = 0; i < kMaxRows; ++i) p.dst_off[i] = L.dst_off[i];
+    for (int j = 0; j < kMaxSrc; ++j)
+        for (int r = 0; r < kMaxBmRows; ++r) p.mask[j][r] = L.mask[j][r];
+    hipLaunchKernelGGL(bm_tail_kernel, dim3((L.n_stripes + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, p);
+    return hipGetLastError();
+}
+
 }  // namespace detail
 
 using namespace detail;
@@ -116,7 +213,7 @@ uint32_t stream_blocks(uint64_t len) {
 hipError_t launch_gf8(const Gf8Launch &L, hipStream_t stream) {
     if (L.k < 1 || L.k > kMaxSrc || L.rows < 1 || L.rows > kMaxRows) return hipErrorInvalidValue;
     if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
-    if (L.len > (uint64_t(UINT32_MAX) - 1) * 16) return hipErrorInvalidValue;
+    if (L.len / 16 > uint64_t(UINT32_MAX)) return hipErrorInvalidValue;
     return kGf8Table[size_t(L.k - 1) * kMaxRows + size_t(L.rows - 1)](L, stream);
 }
 
