@@ -7,9 +7,9 @@
 // computes (jerasure_do_scheduled_operations, jerasure.c:1162-1185) without
 // materialising intermediate packets: each lane keeps its R*W output slices
 // in registers and streams the k*w source slices through once.  The bits
-// are kernel arguments, so every (output, input) pair is a uniform branch
-// around one vector XOR; the next source chunk is loaded while the current
-// one is being combined.
+// are kernel arguments expanded to 0/~0 masks in SGPRs, so every (output,
+// input) pair is one v_bitop3_b32 (acc ^ (d & m)) per dword; the next
+// source chunk is loaded while the current one is being combined.
 #pragma once
 
 #include "stream_common.hpp"
@@ -27,6 +27,18 @@ template <>
 struct VecT<2> {
     typedef u32x2 type;
 };
+
+// (d & m) ^ acc, one v_bitop3_b32 per dword (truth table over
+// src0 = 0xF0, src1 = 0xCC, src2 = 0xAA: (0xF0 & 0xCC) ^ 0xAA = 0x6A).
+__device__ __forceinline__ uint32_t and_xor(uint32_t d, uint32_t m, uint32_t acc) {
+    return uint32_t(__builtin_amdgcn_bitop3_b32(d, m, acc, 0x6A));
+}
+__device__ __forceinline__ u32x4 and_xor(u32x4 d, uint32_t m, u32x4 acc) {
+    return u32x4{and_xor(d.x, m, acc.x), and_xor(d.y, m, acc.y), and_xor(d.z, m, acc.z), and_xor(d.w, m, acc.w)};
+}
+__device__ __forceinline__ u32x2 and_xor(u32x2 d, uint32_t m, u32x2 acc) {
+    return u32x2{and_xor(d.x, m, acc.x), and_xor(d.y, m, acc.y)};
+}
 
 template <int W, int R>
 struct BmParams {
@@ -80,8 +92,12 @@ __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
         for (int r = 0; r < ROWS; ++r) {
             const uint32_t mb = p.mask[j][r];
 #pragma unroll
-            for (int x = 0; x < W; ++x)
-                if ((mb >> x) & 1u) acc[r] ^= d[x];
+            for (int x = 0; x < W; ++x) {
+                // 0 / ~0 from a kernel-argument bit (SALU); acc ^= d & m is one
+                // v_bitop3_b32 per dword on gfx950.
+                const uint32_t m = 0u - ((mb >> x) & 1u);
+                acc[r] = and_xor(d[x], m, acc[r]);
+            }
         }
 #pragma unroll
         for (int x = 0; x < W; ++x) d[x] = nx[x];

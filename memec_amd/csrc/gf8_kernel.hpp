@@ -4,7 +4,7 @@
 // Arithmetic: c*x is linear in the bits of x, so every byte is split into
 // bit fields 0-2 | 3-5 | 6-7 and each field indexes a <= 8-entry table of
 // c*(field << shift) with one v_perm_b32, four bytes per instruction:
-// 3 v_perm + 3 v_xor per (coefficient, dword).  Coefficient 1 is a plain
+// 3 v_perm + 2 v_bitop3 per (coefficient, dword).  Coefficient 1 is a plain
 // XOR and coefficient 0 is skipped (uniform branches on kernel-argument
 // masks).  Replaces the scalar multtable[s][c] byte loop
 // (gf_w8.c:1047-1050) and ISA-L's PSHUFB nibble kernels
@@ -32,6 +32,13 @@ struct Gf8Params {
     int64_t dst_off[R];
     Gf8Coef coef[R][K];
 };
+
+// a ^ b ^ c ^ d in two gfx950 v_bitop3_b32 (truth table 0x96 = 3-input XOR;
+// hipcc does not fuse XOR chains on its own).
+__device__ __forceinline__ uint32_t xor4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const uint32_t t = uint32_t(__builtin_amdgcn_bitop3_b32(a, b, c, 0x96));
+    return uint32_t(__builtin_amdgcn_bitop3_b32(t, d, 0u, 0x96));
+}
 
 __device__ __forceinline__ uint32_t gf8_mul(const Gf8Coef &c, uint32_t x) {
     return __builtin_amdgcn_perm(c.t1, c.t0, x & 0x07070707u) ^
@@ -87,14 +94,14 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
             }
             const u32x4 t = *reinterpret_cast<const u32x4 *>(tb + b * 8);
             const uint32_t v = tb[b * 8 + 4];
-            acc[i].x ^= __builtin_amdgcn_perm(t.y, t.x, s0.x) ^ __builtin_amdgcn_perm(t.w, t.z, s1.x) ^
-                        __builtin_amdgcn_perm(v, v, s2.x);
-            acc[i].y ^= __builtin_amdgcn_perm(t.y, t.x, s0.y) ^ __builtin_amdgcn_perm(t.w, t.z, s1.y) ^
-                        __builtin_amdgcn_perm(v, v, s2.y);
-            acc[i].z ^= __builtin_amdgcn_perm(t.y, t.x, s0.z) ^ __builtin_amdgcn_perm(t.w, t.z, s1.z) ^
-                        __builtin_amdgcn_perm(v, v, s2.z);
-            acc[i].w ^= __builtin_amdgcn_perm(t.y, t.x, s0.w) ^ __builtin_amdgcn_perm(t.w, t.z, s1.w) ^
-                        __builtin_amdgcn_perm(v, v, s2.w);
+            acc[i].x = xor4(acc[i].x, __builtin_amdgcn_perm(t.y, t.x, s0.x), __builtin_amdgcn_perm(t.w, t.z, s1.x),
+                            __builtin_amdgcn_perm(v, v, s2.x));
+            acc[i].y = xor4(acc[i].y, __builtin_amdgcn_perm(t.y, t.x, s0.y), __builtin_amdgcn_perm(t.w, t.z, s1.y),
+                            __builtin_amdgcn_perm(v, v, s2.y));
+            acc[i].z = xor4(acc[i].z, __builtin_amdgcn_perm(t.y, t.x, s0.z), __builtin_amdgcn_perm(t.w, t.z, s1.z),
+                            __builtin_amdgcn_perm(v, v, s2.z));
+            acc[i].w = xor4(acc[i].w, __builtin_amdgcn_perm(t.y, t.x, s0.w), __builtin_amdgcn_perm(t.w, t.z, s1.w),
+                            __builtin_amdgcn_perm(v, v, s2.w));
         }
     }
 #pragma unroll
