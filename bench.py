@@ -106,15 +106,16 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory (PCIe) batch encode")
+    ap.add_argument("--strong", action="store_true",
+                    help="--stripes is the global batch, sharded over ranks (default: per-GPU batch, weak scaling)")
     args = ap.parse_args()
 
     import torch
     import torch.distributed as dist
     from memec_amd import Codec, fill_random
+    from memec_amd.shard import dist_env, shard_range, timed_steps
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = dist_env()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -123,6 +124,11 @@ def main():
     fam, k, m, cs, stripes, op, erased = CONFIGS[args.config]
     if args.stripes:
         stripes = args.stripes
+    global_stripes = stripes * world
+    if args.strong:  # fixed total batch, partitioned by stripe ranges
+        global_stripes = stripes
+        s0, s1 = shard_range(stripes, rank, world)
+        stripes = s1 - s0
     codec = Codec(fam, k, m, cs, device=local)
     seed = 0x4D454D4543 + rank
 
@@ -148,31 +154,10 @@ def main():
         def step():
             codec.decode(stripe, present)
         alg_bytes = (k + len(erased)) * cs * stripes
-    data_bytes = k * cs * stripes
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record()
-    for _ in range(args.steps):
-        step()
-    ev1.record()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    wall = t1 - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step
-    if world > 1:
-        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall, kern_ms = float(tt[0]), float(tt[1])
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    wall, kern_ms = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize,
+                                dist=dist if world > 1 else None, events=ev)  # one launch per step
 
     ok = None
     if op == "decode" and orig is not None:
@@ -208,7 +193,7 @@ def main():
         e2e = {"unit": "GiB/s data (H2D data + kernel + D2H parity)", "stripes": n, **res}
 
     if rank == 0:
-        value = world * data_bytes * args.steps / wall / 2**30
+        value = global_stripes * k * cs * args.steps / wall / 2**30
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         line = {
             "metric": METRIC,
@@ -219,12 +204,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 stripes generated in HBM)",
             "config": {"workload": WORKLOAD_NAMES[args.config], "family": fam, "k": k, "m": m,
-                       "chunk_bytes": cs, "stripes_per_gpu": stripes, "global_stripes": stripes * world,
+                       "chunk_bytes": cs, "stripes_per_gpu": stripes, "global_stripes": global_stripes,
                        "op": op, "erased": erased, "parallelism": "stripe-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),

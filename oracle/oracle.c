@@ -414,19 +414,20 @@ fail:
 /* Region primitives                                                         */
 /* ------------------------------------------------------------------------ */
 
-/* gf_multby_one with xor (gf.c:894-989): 64-bit words, byte tails. */
+/* gf_multby_one with xor (gf.c:894-989): bytes up to 8-byte alignment of
+ * dst, then 64-bit words (gf.c:974-978), then a byte tail. */
 static void region_xor(const uint8_t *src, uint8_t *dst, size_t n)
 {
-    size_t i = 0;
-    while (i < n && ((uintptr_t)(dst + i) & 7)) { dst[i] ^= src[i]; i++; }
-    for (; i + 8 <= n; i += 8) {
-        uint64_t a, b;
-        memcpy(&a, src + i, 8);
-        memcpy(&b, dst + i, 8);
-        b ^= a;
-        memcpy(dst + i, &b, 8);
-    }
-    for (; i < n; i++) dst[i] ^= src[i];
+    size_t head = (8 - ((uintptr_t)dst & 7)) & 7, i, words;
+    const uint64_t *s64;
+    uint64_t *d64;
+    if (head > n) head = n;
+    for (i = 0; i < head; i++) dst[i] ^= src[i];
+    words = (n - head) / 8;
+    s64 = (const uint64_t *)(src + head);
+    d64 = (uint64_t *)(dst + head);
+    for (i = 0; i < words; i++) d64[i] ^= s64[i];
+    for (i = head + words * 8; i < n; i++) dst[i] ^= src[i];
 }
 
 void orc_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, size_t len)

@@ -148,3 +148,20 @@ int ref_invert_matrix(int *mat, int *inv, int n, int w) { return jerasure_invert
 int ref_invert_bitmatrix(int *mat, int *inv, int n) { return jerasure_invert_bitmatrix(mat, inv, n); }
 
 }  // extern "C"
+
+// Timing entry points (tools/speed_fidelity.py): chunks allocated once, so
+// a timed encode is exactly one Coding::encode call on resident chunks.
+extern "C" {
+void *ref_alloc_chunks(uint32_t n) {
+    Chunk **c = new Chunk *[n];
+    TempChunkPool pool;
+    for (uint32_t i = 0; i < n; i++) c[i] = pool.alloc();
+    return c;
+}
+char *ref_chunk_data(void *chunks, uint32_t i) { return ChunkUtil::getData(((Chunk **)chunks)[i]); }
+void ref_encode_chunks(void *hp, void *chunks, uint32_t first, uint32_t index) {
+    RefHandle *h = (RefHandle *)hp;
+    Chunk **c = (Chunk **)chunks + first;
+    h->coding->encode(c, c[h->k + index - 1], index);
+}
+}

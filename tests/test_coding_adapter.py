@@ -1,0 +1,47 @@
+"""The C++ drop-in for MemEC's `class Coding` (memec_amd/csrc/coding/):
+build it standalone like server/ would link it (CPU), then run the
+coding_test program (tests/cpp/coding_test.cc, the reference's own coding
+test flow) against the GPU (gpu)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CODING = os.path.join(ROOT, "memec_amd", "csrc", "coding")
+
+
+def _build(tmpdir, isal):
+    out = os.path.join(str(tmpdir), "coding_test_isal" if isal else "coding_test")
+    srcs = [os.path.join(CODING, f) for f in sorted(os.listdir(CODING)) if f.endswith(".cc")]
+    cmd = ["g++", "-std=c++11", "-O2", "-Wall", "-Werror", "-I" + CODING, "-I" + os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "cpp", "coding_test.cc")] + srcs + \
+          ["-L" + os.path.join(ROOT, "memec_amd"), "-lmec", "-Wl,-rpath," + os.path.join(ROOT, "memec_amd"),
+           "-lpthread", "-o", out]
+    if isal:
+        cmd.insert(1, "-DUSE_ISAL")
+    subprocess.check_call(cmd)
+    return out
+
+
+@pytest.fixture(scope="module")
+def binaries(tmp_path_factory):
+    d = tmp_path_factory.mktemp("coding")
+    return _build(d, False), _build(d, True)
+
+
+def test_adapter_builds_standalone(binaries):
+    for b in binaries:
+        assert os.path.exists(b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    ["rs"], ["cauchy"], ["rs", "10", "4", "65536"], ["cauchy", "12", "4", "65536"],
+    ["rs", "4", "2", "4096"], ["cauchy", "4", "2", "96"], ["rs", "20", "12", "1032"],
+])
+def test_coding_flow_on_gpu(binaries, args):
+    for b in binaries:
+        r = subprocess.run([b] + args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (b, args, r.stdout, r.stderr)
+        assert ": ok" in r.stdout
