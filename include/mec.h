@@ -27,6 +27,20 @@
  *   mec_encode_update_host       C++ Coding adapter (memec_amd/csrc/coding/)
  *                                forwards its virtual methods here
  *   mec_encode_host_batch        host-memory (PCIe-inclusive) batched encode
+ *   mec_encode_batch /           the libmec batch ABI of SURVEY §8(b): many
+ *   mec_decode_batch /           stripes given as per-stripe chunk pointer
+ *   mec_encode_update_batch      rows (Chunk** as server/ holds them), device
+ *                                or host memory; replaces a loop of
+ *                                Coding::encode / Coding::decode calls
+ *                                (parity_chunk_buffer.cc:349, worker.cc:49,
+ *                                server_peer_res_worker.cc:836-838) and the
+ *                                server's delta encodes
+ *                                (parity_chunk_buffer.cc:342-353,
+ *                                degraded_chunk_buffer.cc:645-656)
+ *   mec_set_coalescing           batching of concurrent mec_*_host calls from
+ *                                the server's worker threads, which share one
+ *                                Coding instance (server.cc:107,
+ *                                worker.cc:128-137)
  *
  * Memory: the device entry points take device pointers (hipMalloc / torch
  * CUDA tensors) and a hipStream_t passed as void* (NULL = default stream);
@@ -79,7 +93,18 @@ typedef enum {
     MEC_ISAL_CAUCHY = 3
 } mec_family;
 
+typedef enum {
+    MEC_MEM_DEVICE = 0, /* device pointers; asynchronous on the given stream */
+    MEC_MEM_HOST = 1    /* host pointers (pageable or registered); synchronous */
+} mec_mem_kind;
+
 typedef struct mec_ctx mec_ctx;
+
+typedef struct {
+    uint64_t coalesced_batches;  /* batches run by the coalescer */
+    uint64_t coalesced_requests; /* single-stripe requests they carried */
+    uint64_t cached_plans;       /* decode plans cached (one per erasure pattern) */
+} mec_stats;
 
 typedef struct {
     int32_t family;
@@ -175,6 +200,50 @@ int mec_encode_host_batch(mec_ctx *ctx, const uint8_t *data, uint8_t *parity,
                           uint32_t n_stripes, uint32_t parity_mask);
 int mec_host_register(void *ptr, size_t len);
 int mec_host_unregister(void *ptr);
+
+/* ---- pointer-array batches ------------------------------------------------
+ *
+ * A batch is n_stripes rows of chunk pointers, row-major (stripe s's chunk
+ * c at array[s * chunks_per_row + c]), as the server holds Chunk* arrays.
+ * mem_kind MEC_MEM_DEVICE: device pointers, work enqueued on `stream`
+ * (the pointer arrays themselves are host arrays, consumed before return).
+ * MEC_MEM_HOST: host pointers (pageable, or registered with
+ * mec_host_register); staged through HBM, synchronous, `stream` ignored.
+ * Stripes are grouped by their linear map (same sources / outputs); each
+ * group is one gather launch. */
+
+/* data: n_stripes * k pointers, NULL = the all-zero Coding::zeros chunk
+ * (neither read nor multiplied).  parity: n_stripes * m pointers, NULL = not
+ * wanted; parity_mask (0 = all m) filters further.  Wanted parities are
+ * overwritten. */
+int mec_encode_batch(mec_ctx *ctx, const uint8_t *const *data, uint8_t *const *parity, uint32_t n_stripes,
+                     uint32_t parity_mask, int mem_kind, void *stream);
+
+/* chunks: n_stripes * (k + m) pointers; present_masks[s] bit i set <=> chunk
+ * i of stripe s is present.  Each stripe's missing chunks are rebuilt in
+ * place exactly as mec_decode would (the reference's survivors and decoding
+ * matrix); stripes may have different erasure patterns.  results (optional,
+ * n_stripes entries) receives each stripe's status: MEC_OK or
+ * MEC_ETOOMANY (more than m missing; the reference's decode() == false) /
+ * MEC_EINVAL.  Decodable stripes are decoded even when others fail; the
+ * return value is the first failure, or MEC_OK. */
+int mec_decode_batch(mec_ctx *ctx, uint8_t *const *chunks, const uint64_t *present_masks, uint32_t n_stripes,
+                     int32_t *results, int mem_kind, void *stream);
+
+/* Delta encode: parity[s * m + i] ^= A[i][data_index[s]] * delta[s] for every
+ * non-NULL parity pointer in parity_mask (0 = all).  delta[s] == NULL is an
+ * all-zero delta (no work). */
+int mec_encode_update_batch(mec_ctx *ctx, const uint32_t *data_index, const uint8_t *const *delta,
+                            uint8_t *const *parity, uint32_t n_stripes, uint32_t parity_mask, int mem_kind,
+                            void *stream);
+
+/* Coalesce concurrent mec_encode_host / mec_decode_host /
+ * mec_encode_update_host calls on this context: while one batch runs,
+ * arriving calls queue, and the next caller to lead takes up to max_batch
+ * of them as one host batch.  An idle context adds no wait.  0 = off
+ * (default): every call is its own launch. */
+int mec_set_coalescing(mec_ctx *ctx, uint32_t max_batch);
+int mec_get_stats(const mec_ctx *ctx, mec_stats *out);
 
 #ifdef __cplusplus
 }

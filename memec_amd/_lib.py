@@ -19,7 +19,9 @@ SYMBOLS = (
     "mec_get_matrix", "mec_get_bitmatrix", "mec_encode", "mec_decode", "mec_decode_split",
     "mec_encode_update", "mec_xor", "mec_fill_random", "mec_encode_host", "mec_decode_host",
     "mec_encode_update_host", "mec_encode_host_batch", "mec_host_register", "mec_host_unregister",
+    "mec_encode_batch", "mec_decode_batch", "mec_encode_update_batch", "mec_set_coalescing", "mec_get_stats",
 )
+MEM_DEVICE, MEM_HOST = 0, 1
 
 
 class MecError(RuntimeError):
@@ -32,6 +34,11 @@ class MecInfo(ctypes.Structure):
     _fields_ = [("family", ctypes.c_int32), ("k", ctypes.c_uint32), ("m", ctypes.c_uint32),
                 ("w", ctypes.c_uint32), ("chunk_size", ctypes.c_uint32),
                 ("packet_size", ctypes.c_uint32), ("device", ctypes.c_int32)]
+
+
+class MecStats(ctypes.Structure):
+    _fields_ = [("coalesced_batches", ctypes.c_uint64), ("coalesced_requests", ctypes.c_uint64),
+                ("cached_plans", ctypes.c_uint64)]
 
 
 _lib = None
@@ -69,6 +76,13 @@ def lib():
     L.mec_encode_host_batch.argtypes = [vp, vp, vp, u32, u32]
     L.mec_host_register.argtypes = [vp, ctypes.c_size_t]
     L.mec_host_unregister.argtypes = [vp]
+    pvp = ctypes.POINTER(vp)
+    L.mec_encode_batch.argtypes = [vp, pvp, pvp, u32, u32, ctypes.c_int, vp]
+    L.mec_decode_batch.argtypes = [vp, pvp, ctypes.POINTER(u64), u32, ctypes.POINTER(ctypes.c_int32),
+                                   ctypes.c_int, vp]
+    L.mec_encode_update_batch.argtypes = [vp, ctypes.POINTER(u32), pvp, pvp, u32, u32, ctypes.c_int, vp]
+    L.mec_set_coalescing.argtypes = [vp, u32]
+    L.mec_get_stats.argtypes = [vp, ctypes.POINTER(MecStats)]
     _lib = L
     return L
 

@@ -132,6 +132,68 @@ class Codec:
                                           data.shape[0], parity_mask))
 
 
+    # ---- pointer-array batches (any memory kind) ----------------------------------
+    # Pointers are integers (0 = NULL), one row per stripe: k data / m parity
+    # for encode, k + m chunks for decode.  mem: "device" (CUDA tensor
+    # addresses, enqueued on the stream) or "host" (numpy addresses; staged
+    # through HBM, synchronous).
+    @staticmethod
+    def _ptr_array(ptrs):
+        """uint64 numpy array (zero-copy) or a sequence of ints -> (void**, keepalive)."""
+        a = np.ascontiguousarray(np.asarray(ptrs, dtype=np.uint64))
+        return ctypes.cast(a.ctypes.data, ctypes.POINTER(vp)), a
+
+    @staticmethod
+    def _mem(mem):
+        return {"device": _lib.MEM_DEVICE, "host": _lib.MEM_HOST}[mem]
+
+    def _stream_for(self, mem, stream):
+        return _stream(stream) if mem == "device" else vp()
+
+    def encode_batch(self, data_ptrs, parity_ptrs, parity_mask=0, mem="device", stream=None):
+        n = len(data_ptrs) // self.k
+        if len(data_ptrs) != n * self.k or len(parity_ptrs) != n * self.m:
+            raise ValueError("need n*k data and n*m parity pointers")
+        dp, _a = self._ptr_array(data_ptrs)
+        pp, _b = self._ptr_array(parity_ptrs)
+        check(lib().mec_encode_batch(self._h, dp, pp, n, parity_mask, self._mem(mem), self._stream_for(mem, stream)))
+
+    def decode_batch(self, chunk_ptrs, present_masks, mem="device", stream=None):
+        """Returns the per-stripe status list (0 ok, MEC_ETOOMANY, ...)."""
+        n = len(present_masks)
+        if len(chunk_ptrs) != n * (self.k + self.m):
+            raise ValueError("need n*(k+m) chunk pointers")
+        cp, _a = self._ptr_array(chunk_ptrs)
+        pmv = np.ascontiguousarray(np.asarray(present_masks, dtype=np.uint64))
+        pm = ctypes.cast(pmv.ctypes.data, ctypes.POINTER(_lib.u64))
+        res = (ctypes.c_int32 * n)()
+        rc = lib().mec_decode_batch(self._h, cp, pm, n, res, self._mem(mem), self._stream_for(mem, stream))
+        out = list(res)
+        if rc < 0 and rc not in out:  # a failure not attributable to one stripe
+            check(rc)
+        return out
+
+    def encode_update_batch(self, data_index, delta_ptrs, parity_ptrs, parity_mask=0, mem="device", stream=None):
+        n = len(data_index)
+        if len(delta_ptrs) != n or len(parity_ptrs) != n * self.m:
+            raise ValueError("need n deltas and n*m parity pointers")
+        div = np.ascontiguousarray(np.asarray(data_index, dtype=np.uint32))
+        di = ctypes.cast(div.ctypes.data, ctypes.POINTER(_lib.u32))
+        dp, _a = self._ptr_array(delta_ptrs)
+        pp, _b = self._ptr_array(parity_ptrs)
+        check(lib().mec_encode_update_batch(self._h, di, dp, pp, n, parity_mask, self._mem(mem),
+                                            self._stream_for(mem, stream)))
+
+    def set_coalescing(self, max_batch):
+        check(lib().mec_set_coalescing(self._h, max_batch))
+
+    def stats(self):
+        st = _lib.MecStats()
+        check(lib().mec_get_stats(self._h, ctypes.byref(st)))
+        return {"coalesced_batches": st.coalesced_batches, "coalesced_requests": st.coalesced_requests,
+                "cached_plans": st.cached_plans}
+
+
 def fill_random(t, seed, word_offset=0, stream=None):
     """Fill a contiguous uint8 CUDA tensor with the splitmix64 stream."""
     if not t.is_cuda or not t.is_contiguous():

@@ -1,0 +1,209 @@
+// ctx.hpp — libmec internals shared by mec.cpp (lifecycle, strided entry
+// points, single-stripe host staging) and batch.cpp (pointer-table batches,
+// host pipeline, request coalescer).  Not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "gf_math.hpp"
+#include "kernels.hpp"
+#include "mec.h"
+
+namespace mec {
+namespace core {
+
+using mec::Field;
+using mec::Mat;
+
+// Thread-local error text (mec_last_error) and status helpers.
+extern thread_local std::string g_err;
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int hip_fail(hipError_t e, const char *what);
+
+#define HIP_TRY(expr)                                     \
+    do {                                                  \
+        hipError_t e_ = (expr);                           \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+// Restores the caller's current device on scope exit.
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// Staging resources for the single-stripe host entry points (one per
+// concurrent caller; server workers share one context, worker.cc:128-137).
+struct Lane {
+    hipStream_t stream = nullptr;
+    uint8_t *dev = nullptr;  // (k + m) chunk slots
+    size_t bytes = 0;
+};
+
+// Pinned host + device copy of a gather table (per-stripe chunk pointers)
+// for the device-memory pointer batches.  `done` is recorded after the last
+// launch that reads it; the slot is reused only after it fired.
+struct TableSlot {
+    std::mutex mu;
+    uint64_t *host = nullptr;
+    uint64_t *dev = nullptr;
+    size_t cap = 0;  // entries
+    hipEvent_t done = nullptr;
+    bool pending = false;
+};
+constexpr int kTableSlots = 4;
+
+// Double-buffered host pipeline of the host-memory pointer batches: chunks
+// are packed into pinned staging, moved with one DMA per sub-batch, coded
+// in HBM, and unpacked from pinned staging.
+struct HostPipe {
+    std::mutex mu;
+    hipStream_t stream[2] = {nullptr, nullptr};
+    hipEvent_t done[2] = {nullptr, nullptr};
+    uint8_t *host[2] = {nullptr, nullptr};
+    uint8_t *dev[2] = {nullptr, nullptr};
+    size_t bytes = 0;  // per buffer
+};
+
+// One pending single-stripe host request (mec_*_host while coalescing).
+struct Request;
+
+struct Coalescer {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Request *> queue;
+    bool leader_active = false;
+    uint32_t max_batch = 0;  // 0 = coalescing off
+    uint64_t batches = 0, requests = 0;  // statistics
+};
+
+}  // namespace core
+}  // namespace mec
+
+struct mec_ctx {
+    int family;
+    uint32_t k, m, w, cs, packet;
+    int device;
+    mec::Mat A;  // m x k (Jerasure) or (k+m) x k (ISA-L)
+    std::mutex plan_mu;
+    std::unordered_map<uint64_t, std::shared_ptr<mec::LinearPlan>> plans;
+    std::mutex lane_mu;
+    std::vector<mec::core::Lane *> lanes_free;
+    std::vector<mec::core::Lane *> lanes_all;
+    // pipelined dense host batch (mec_encode_host_batch)
+    std::mutex batch_mu;
+    hipStream_t bstream[2] = {nullptr, nullptr};
+    uint8_t *bdev[2] = {nullptr, nullptr};
+    size_t bbytes = 0;
+    // pointer batches (batch.cpp)
+    std::mutex tab_mu;
+    uint32_t tab_next = 0;
+    mec::core::TableSlot tabs[mec::core::kTableSlots];
+    mec::core::HostPipe pipe;
+    mec::core::Coalescer coal;
+
+    bool byte_wise() const { return family != MEC_CAUCHY_GOOD; }
+    mec::Scheme scheme() const {
+        return family == MEC_RS_VANDERMONDE ? mec::Scheme::kJerasureRS
+               : family == MEC_CAUCHY_GOOD  ? mec::Scheme::kJerasureCauchy
+                                            : mec::Scheme::kIsal;
+    }
+    // coefficient of parity row i (0..m-1), data column j
+    uint8_t coef(uint32_t i, uint32_t j) const {
+        return byte_wise() && family != MEC_RS_VANDERMONDE ? A[size_t(k + i) * k + j] : A[size_t(i) * k + j];
+    }
+};
+
+namespace mec {
+namespace core {
+
+inline bool has_device(const mec_ctx *c) { return c->device >= 0; }
+
+#define CHECK_CTX(c)                                                          \
+    do {                                                                      \
+        if (!(c)) return fail(MEC_EINVAL, "null context");                    \
+        if (!has_device(c)) return fail(MEC_ENODEV, "context has no device"); \
+    } while (0)
+
+// Where a launch finds its chunks: strided (base + stripe * stride +
+// offset) or gathered from a device table of per-stripe chunk pointers.
+struct Layout {
+    const uint8_t *src = nullptr;
+    uint8_t *dst = nullptr;
+    int64_t sss = 0, dss = 0;
+    std::vector<int64_t> src_off, dst_off;  // strided: one per source / output
+    const uint64_t *tab = nullptr;          // gather: rows [ns sources | nd outputs]
+    uint32_t tstride = 0;
+    size_t ns = 0, nd = 0;
+
+    static Layout strided(const uint8_t *src, int64_t sss, std::vector<int64_t> so, uint8_t *dst, int64_t dss,
+                          std::vector<int64_t> dof) {
+        Layout l;
+        l.src = src;
+        l.dst = dst;
+        l.sss = sss;
+        l.dss = dss;
+        l.ns = so.size();
+        l.nd = dof.size();
+        l.src_off = std::move(so);
+        l.dst_off = std::move(dof);
+        return l;
+    }
+    static Layout gather(const uint64_t *tab, size_t ns, size_t nd) {
+        Layout l;
+        l.tab = tab;
+        l.tstride = uint32_t(ns + nd);
+        l.ns = ns;
+        l.nd = nd;
+        return l;
+    }
+};
+
+void bit_block(const Field &f, unsigned e, uint32_t w, uint8_t *mask, size_t mstride);
+// outputs (^)= coef (nd x ns over GF(2^w)) * sources, every stripe.
+int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bool accumulate, hipStream_t stream);
+int apply(mec_ctx *c, const uint8_t *src, int64_t sss, const std::vector<int64_t> &src_off, uint8_t *dst,
+          int64_t dss, const std::vector<int64_t> &dst_off, const Mat &coef, uint32_t n_stripes, bool accumulate,
+          hipStream_t stream);
+// Cached decode plan for a present-chunk mask (reference survivor choice).
+int get_plan(mec_ctx *c, uint64_t present, std::shared_ptr<mec::LinearPlan> &out);
+Mat encode_rows(const mec_ctx *c, const std::vector<uint32_t> &rows, const std::vector<uint32_t> &cols);
+std::vector<uint32_t> mask_rows(const mec_ctx *c, uint32_t parity_mask);
+Lane *lane_acquire(mec_ctx *c, int &rc);
+void lane_release(mec_ctx *c, Lane *l);
+
+struct LaneHold {
+    mec_ctx *c;
+    Lane *l;
+    ~LaneHold() {
+        if (l) lane_release(c, l);
+    }
+};
+
+// batch.cpp
+void batch_release(mec_ctx *c);  // frees table slots and the host pipeline
+bool coalescing(mec_ctx *c);
+int submit_encode(mec_ctx *c, const uint8_t *const *data, uint8_t *const *parity);
+int submit_decode(mec_ctx *c, uint8_t *const *chunks, uint64_t present);
+int submit_update(mec_ctx *c, uint32_t index, const uint8_t *delta, uint8_t *const *parity);
+
+}  // namespace core
+}  // namespace mec

@@ -26,6 +26,8 @@ struct Gf8Params {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
+    const uint64_t *tab;  // gather mode: per stripe [K sources | dsts] chunk pointers
+    uint32_t tstride, tdst;
     uint32_t units, tiles, accumulate, pad;
     uint32_t ones[4], zeros[4];  // bit i*K+j: coefficient (i, j) is 1 / 0
     int64_t src_off[K];
@@ -46,7 +48,9 @@ __device__ __forceinline__ uint32_t gf8_mul(const Gf8Coef &c, uint32_t x) {
            __builtin_amdgcn_perm(c.v, c.v, (x >> 6) & 0x03030303u);
 }
 
-template <int K, int R>
+// G = gather: chunk addresses come from a per-stripe pointer table (scalar
+// loads, uniform per block) instead of base + stripe * stride + offset.
+template <int K, int R, bool G>
 __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) {
     __shared__ uint32_t tab[R * K * 8];
     for (int t = threadIdx.x; t < R * K; t += kThreads) {
@@ -62,16 +66,37 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
     const uint32_t u = (blockIdx.x - stripe * p.tiles) * kThreads + threadIdx.x;
     if (u >= p.units) return;
     const uint64_t off = uint64_t(u) * 16;
-    const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
-    uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
+    const uint8_t *sb = nullptr;
+    uint8_t *db = nullptr;
+    const uint64_t *row = nullptr;
+    if constexpr (G) {
+        row = p.tab + uint64_t(stripe) * p.tstride;
+    } else {
+        sb = p.src + int64_t(stripe) * p.sss + off;
+        db = p.dst + int64_t(stripe) * p.dss + off;
+    }
+    // kept as address expressions at the use sites: materialising pointer
+    // arrays costs the strided kernel 6 VGPRs and a wave per SIMD
+    auto sp = [&](int j) -> const uint8_t * {
+        if constexpr (G)
+            return reinterpret_cast<const uint8_t *>(row[j]) + off;
+        else
+            return sb + p.src_off[j];
+    };
+    auto dp = [&](int i) -> uint8_t * {
+        if constexpr (G)
+            return reinterpret_cast<uint8_t *>(row[p.tdst + i]) + off;
+        else
+            return db + p.dst_off[i];
+    };
 
     u32x4 d[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) d[j] = ld_nt<u32x4>(sb + p.src_off[j]);
+    for (int j = 0; j < K; ++j) d[j] = ld_nt<u32x4>(sp(j));
     u32x4 acc[R];
     if (p.accumulate) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) acc[i] = *reinterpret_cast<const u32x4 *>(db + p.dst_off[i]);
+        for (int i = 0; i < R; ++i) acc[i] = *reinterpret_cast<const u32x4 *>(dp(i));
     } else {
 #pragma unroll
         for (int i = 0; i < R; ++i) acc[i] = u32x4{0, 0, 0, 0};
@@ -105,7 +130,7 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
         }
     }
 #pragma unroll
-    for (int i = 0; i < R; ++i) st_nt<u32x4>(db + p.dst_off[i], acc[i]);
+    for (int i = 0; i < R; ++i) st_nt<u32x4>(dp(i), acc[i]);
 }
 
 // The < 16-byte remainder of each region (chunk sizes that are not a
@@ -114,6 +139,8 @@ struct Gf8TailParams {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
+    const uint64_t *tab;
+    uint32_t tstride, tdst;
     uint64_t off;
     uint32_t n, k, rows, n_stripes, accumulate, pad;
     int64_t src_off[kMaxSrc];
@@ -128,6 +155,8 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     Gf8Params<K, R> p;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
+    p.tstride = L.tab_stride;
+    p.tdst = L.tab_dst;
     const Geometry g = geometry(L.len / 16);
     p.units = g.units;
     p.tiles = g.tiles;
@@ -146,9 +175,17 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     if (g.units > 0) {
         for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-            p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-            p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-            hipLaunchKernelGGL((gf8_kernel<K, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            if (L.tab) {
+                p.src = nullptr;
+                p.dst = nullptr;
+                p.tab = L.tab + uint64_t(s0) * L.tab_stride;
+                hipLaunchKernelGGL((gf8_kernel<K, R, true>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            } else {
+                p.src = L.src + int64_t(s0) * L.src_stripe_stride;
+                p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+                p.tab = nullptr;
+                hipLaunchKernelGGL((gf8_kernel<K, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
@@ -157,39 +194,14 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     return hipSuccess;
 }
 
-#define MEC_GF8_INSTANTIATE_K(R) \
-    template hipError_t run_gf8<1, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<2, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<3, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<4, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<5, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<6, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<7, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<8, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<9, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<10, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<11, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<12, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<13, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<14, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<15, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<16, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<17, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<18, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<19, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<20, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<21, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<22, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<23, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<24, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<25, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<26, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<27, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<28, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<29, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<30, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<31, R>(const Gf8Launch &, hipStream_t); \
-    template hipError_t run_gf8<32, R>(const Gf8Launch &, hipStream_t);
+#define MEC_GF8_ONE(K, R) template hipError_t run_gf8<K, R>(const Gf8Launch &, hipStream_t);
+// K = 1..16 and 17..32 in separate translation units (parallel builds).
+#define MEC_GF8_INSTANTIATE_LO(R) \
+    MEC_GF8_ONE(1, R) MEC_GF8_ONE(2, R) MEC_GF8_ONE(3, R) MEC_GF8_ONE(4, R) MEC_GF8_ONE(5, R) MEC_GF8_ONE(6, R) MEC_GF8_ONE(7, R) MEC_GF8_ONE(8, R) \
+    MEC_GF8_ONE(9, R) MEC_GF8_ONE(10, R) MEC_GF8_ONE(11, R) MEC_GF8_ONE(12, R) MEC_GF8_ONE(13, R) MEC_GF8_ONE(14, R) MEC_GF8_ONE(15, R) MEC_GF8_ONE(16, R)
+#define MEC_GF8_INSTANTIATE_HI(R) \
+    MEC_GF8_ONE(17, R) MEC_GF8_ONE(18, R) MEC_GF8_ONE(19, R) MEC_GF8_ONE(20, R) MEC_GF8_ONE(21, R) MEC_GF8_ONE(22, R) MEC_GF8_ONE(23, R) MEC_GF8_ONE(24, R) \
+    MEC_GF8_ONE(25, R) MEC_GF8_ONE(26, R) MEC_GF8_ONE(27, R) MEC_GF8_ONE(28, R) MEC_GF8_ONE(29, R) MEC_GF8_ONE(30, R) MEC_GF8_ONE(31, R) MEC_GF8_ONE(32, R)
 
 }  // namespace detail
 }  // namespace mec

@@ -1,0 +1,8 @@
+// gf8_r3hi.hip — GF(2^8) kernel instantiations with 3 output row(s), K = 17..32.
+#include "gf8_kernel.hpp"
+
+namespace mec {
+namespace detail {
+MEC_GF8_INSTANTIATE_HI(3)
+}  // namespace detail
+}  // namespace mec

@@ -42,16 +42,21 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream);
 __global__ __launch_bounds__(kThreads) void gf8_tail_kernel(const Gf8TailParams p) {
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
     if (s >= p.n_stripes) return;
-    const uint8_t *sb = p.src + int64_t(s) * p.sss + p.off;
-    uint8_t *db = p.dst + int64_t(s) * p.dss + p.off;
+    const uint64_t *row = p.tab ? p.tab + uint64_t(s) * p.tstride : nullptr;
+    auto srcp = [&](uint32_t j) -> const uint8_t * {
+        return row ? reinterpret_cast<const uint8_t *>(row[j]) + p.off : p.src + int64_t(s) * p.sss + p.off + p.src_off[j];
+    };
+    auto dstp = [&](uint32_t i) -> uint8_t * {
+        return row ? reinterpret_cast<uint8_t *>(row[p.tdst + i]) + p.off : p.dst + int64_t(s) * p.dss + p.off + p.dst_off[i];
+    };
     for (uint32_t i = 0; i < p.rows; ++i) {
-        u32x4 acc = p.accumulate ? load_partial(db + p.dst_off[i], p.n) : u32x4{0, 0, 0, 0};
+        u32x4 acc = p.accumulate ? load_partial(dstp(i), p.n) : u32x4{0, 0, 0, 0};
         for (uint32_t j = 0; j < p.k; ++j) {
-            const u32x4 x = load_partial(sb + p.src_off[j], p.n);
+            const u32x4 x = load_partial(srcp(j), p.n);
             const Gf8Coef c = p.coef[i][j];
             acc ^= u32x4{gf8_mul(c, x.x), gf8_mul(c, x.y), gf8_mul(c, x.z), gf8_mul(c, x.w)};
         }
-        store_partial(db + p.dst_off[i], acc, p.n);
+        store_partial(dstp(i), acc, p.n);
     }
 }
 
@@ -61,6 +66,9 @@ hipError_t launch_gf8_tail(const Gf8Launch &L, uint64_t off, hipStream_t stream)
     p.dst = L.dst;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
+    p.tab = L.tab;
+    p.tstride = L.tab_stride;
+    p.tdst = L.tab_dst;
     p.off = off;
     p.n = uint32_t(L.len - off);
     p.k = uint32_t(L.k);
@@ -81,6 +89,8 @@ struct BmTailParams {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
+    const uint64_t *tab;
+    uint32_t tstride, tdst;
     uint64_t packet, off;
     uint32_t n, k, rows, w, n_stripes, accumulate;
     int64_t src_off[kMaxSrc];
@@ -91,16 +101,21 @@ struct BmTailParams {
 __global__ __launch_bounds__(kThreads) void bm_tail_kernel(const BmTailParams p) {
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
     if (s >= p.n_stripes) return;
-    const uint8_t *sb = p.src + int64_t(s) * p.sss + p.off;
-    uint8_t *db = p.dst + int64_t(s) * p.dss + p.off;
+    const uint64_t *row = p.tab ? p.tab + uint64_t(s) * p.tstride : nullptr;
+    auto srcp = [&](uint32_t j) -> const uint8_t * {
+        return row ? reinterpret_cast<const uint8_t *>(row[j]) + p.off : p.src + int64_t(s) * p.sss + p.off + p.src_off[j];
+    };
+    auto dstp = [&](uint32_t i) -> uint8_t * {
+        return row ? reinterpret_cast<uint8_t *>(row[p.tdst + i]) + p.off : p.dst + int64_t(s) * p.dss + p.off + p.dst_off[i];
+    };
     for (uint32_t i = 0; i < p.rows; ++i)
         for (uint32_t l = 0; l < p.w; ++l) {
-            uint8_t *q = db + p.dst_off[i] + uint64_t(l) * p.packet;
+            uint8_t *q = dstp(i) + uint64_t(l) * p.packet;
             u32x4 acc = p.accumulate ? load_partial(q, p.n) : u32x4{0, 0, 0, 0};
             for (uint32_t j = 0; j < p.k; ++j) {
                 const uint32_t mb = p.mask[j][i * p.w + l];
                 for (uint32_t x = 0; x < p.w; ++x)
-                    if ((mb >> x) & 1u) acc ^= load_partial(sb + p.src_off[j] + uint64_t(x) * p.packet, p.n);
+                    if ((mb >> x) & 1u) acc ^= load_partial(srcp(j) + uint64_t(x) * p.packet, p.n);
             }
             store_partial(q, acc, p.n);
         }
@@ -112,6 +127,9 @@ hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream) {
     p.dst = L.dst;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
+    p.tab = L.tab;
+    p.tstride = L.tab_stride;
+    p.tdst = L.tab_dst;
     p.packet = L.packet;
     p.off = off;
     p.n = uint32_t(L.packet - off);

@@ -19,11 +19,19 @@ struct Gf8Coef {
 };
 Gf8Coef gf8_coef(uint8_t c);
 
+// Chunk addressing of a launch.  Strided: source j of stripe s is
+// src + s * src_stripe_stride + src_off[j] (dst likewise).  Gather (tab !=
+// nullptr, a device array): stripe s's chunk pointers are the row
+// tab[s * tab_stride ...]: sources at [0, k), outputs at [tab_dst, tab_dst +
+// rows); src / dst / strides / offsets are then unused.
+
 // out[r] (^)= sum_j coef[r][j] * src[j]  over GF(2^8), byte-wise.
 struct Gf8Launch {
     const uint8_t *src;
     uint8_t *dst;
     int64_t src_stripe_stride, dst_stripe_stride;
+    const uint64_t *tab;
+    uint32_t tab_stride, tab_dst;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[kMaxRows];
     int k, rows;
@@ -40,6 +48,8 @@ struct BmLaunch {
     const uint8_t *src;
     uint8_t *dst;
     int64_t src_stripe_stride, dst_stripe_stride;
+    const uint64_t *tab;
+    uint32_t tab_stride, tab_dst;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[kMaxRows];
     int k, rows, w;        // rows = output chunks (each w packets)

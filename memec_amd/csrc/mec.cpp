@@ -1,27 +1,15 @@
 // mec.cpp — libmec C ABI (include/mec.h): coding contexts, plan caching,
-// kernel dispatch and host-memory staging.
-#include "mec.h"
+// kernel dispatch, strided device entry points and single-stripe host
+// staging.  Pointer-table batches, the host pipeline and the request
+// coalescer live in batch.cpp.
+#include "ctx.hpp"
 
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
-#include <memory>
-#include <mutex>
-#include <string>
-#include <unordered_map>
-#include <vector>
 
-#include "gf_math.hpp"
-#include "kernels.hpp"
-
-using mec::Field;
-using mec::Mat;
-
-namespace {
+namespace mec {
+namespace core {
 
 thread_local std::string g_err;
 
@@ -39,135 +27,89 @@ int hip_fail(hipError_t e, const char *what) {
     return fail(MEC_EHIP, "%s: %s", what, hipGetErrorString(e));
 }
 
-#define HIP_TRY(expr)                                   \
-    do {                                                \
-        hipError_t e_ = (expr);                         \
-        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
-    } while (0)
-
-// Restores the caller's current device on scope exit.
-struct DeviceGuard {
-    int prev = -1;
-    bool ok = true;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+// Bitmatrix rows of GF(2^w) coefficient e: mask[l] bit x = bit l of e * 2^x
+// (jerasure_matrix_to_bitmatrix, jerasure.c:271-297).
+void bit_block(const Field &f, unsigned e, uint32_t w, uint8_t *mask, size_t mstride) {
+    uint8_t cols[8];
+    for (uint32_t x = 0; x < w; ++x) {
+        cols[x] = uint8_t(e);
+        e = f.mul(e, 2 % f.size());
     }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    for (uint32_t l = 0; l < w; ++l) {
+        uint8_t mb = 0;
+        for (uint32_t x = 0; x < w; ++x) mb |= uint8_t((cols[x] >> l & 1) << x);
+        mask[l * mstride] = mb;
     }
-};
+}
 
-// Staging resources for the host-memory entry points (one per concurrent
-// caller; server workers share one context, worker.cc:128-137).
-struct Lane {
-    hipStream_t stream = nullptr;
-    uint8_t *dev = nullptr;  // (k + m) chunk slots
-    size_t bytes = 0;
-};
-
-}  // namespace
-
-struct mec_ctx {
-    int family;
-    uint32_t k, m, w, cs, packet;
-    int device;
-    Mat A;  // m x k (Jerasure) or (k+m) x k (ISA-L)
-    std::mutex plan_mu;
-    std::unordered_map<uint64_t, std::shared_ptr<mec::LinearPlan>> plans;
-    std::mutex lane_mu;
-    std::vector<Lane *> lanes_free;
-    std::vector<Lane *> lanes_all;
-    // pipelined host batch
-    std::mutex batch_mu;
-    hipStream_t bstream[2] = {nullptr, nullptr};
-    uint8_t *bdev[2] = {nullptr, nullptr};
-    size_t bbytes = 0;
-
-    bool byte_wise() const { return family != MEC_CAUCHY_GOOD; }
-    mec::Scheme scheme() const {
-        return family == MEC_RS_VANDERMONDE ? mec::Scheme::kJerasureRS
-               : family == MEC_CAUCHY_GOOD  ? mec::Scheme::kJerasureCauchy
-                                            : mec::Scheme::kIsal;
-    }
-    // coefficient of parity row i (0..m-1), data column j
-    uint8_t coef(uint32_t i, uint32_t j) const {
-        return byte_wise() && family != MEC_RS_VANDERMONDE ? A[size_t(k + i) * k + j] : A[size_t(i) * k + j];
-    }
-};
-
-namespace {
-
-bool has_device(const mec_ctx *c) { return c->device >= 0; }
-
-// outputs (^)= coef (n_dst x n_src over GF(2^w)) * sources, every stripe.
-int apply(mec_ctx *c, const uint8_t *src, int64_t sss, const std::vector<int64_t> &src_off, uint8_t *dst,
-          int64_t dss, const std::vector<int64_t> &dst_off, const Mat &coef, uint32_t n_stripes, bool accumulate,
-          hipStream_t stream) {
-    const size_t ns = src_off.size(), nd = dst_off.size();
+// outputs (^)= coef (nd x ns over GF(2^w)) * sources, every stripe.
+int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bool accumulate, hipStream_t stream) {
+    const size_t ns = lay.ns, nd = lay.nd;
     if (nd == 0 || n_stripes == 0) return MEC_OK;
     if (ns == 0) {  // all-zero input: outputs are zero (or unchanged when accumulating)
         if (accumulate) return MEC_OK;
+        if (lay.tab) return fail(MEC_EINVAL, "internal: gathered launch without sources");
         for (uint32_t s = 0; s < n_stripes; ++s)
             for (size_t r = 0; r < nd; ++r)
-                HIP_TRY(hipMemsetAsync(dst + int64_t(s) * dss + dst_off[r], 0, c->cs, stream));
+                HIP_TRY(hipMemsetAsync(lay.dst + int64_t(s) * lay.dss + lay.dst_off[r], 0, c->cs, stream));
         return MEC_OK;
     }
     for (size_t r0 = 0; r0 < nd; r0 += mec::kMaxRows) {
         const int rows = int(std::min<size_t>(mec::kMaxRows, nd - r0));
         if (c->byte_wise()) {
             mec::Gf8Launch L{};
-            L.src = src;
-            L.dst = dst;
-            L.src_stripe_stride = sss;
-            L.dst_stripe_stride = dss;
+            L.src = lay.src;
+            L.dst = lay.dst;
+            L.src_stripe_stride = lay.sss;
+            L.dst_stripe_stride = lay.dss;
+            L.tab = lay.tab;
+            L.tab_stride = lay.tstride;
+            L.tab_dst = uint32_t(ns + r0);
             L.k = int(ns);
             L.rows = rows;
             L.len = c->cs;
             L.n_stripes = n_stripes;
             L.accumulate = accumulate;
-            for (size_t j = 0; j < ns; ++j) L.src_off[j] = src_off[j];
-            for (int i = 0; i < rows; ++i) {
-                L.dst_off[i] = dst_off[r0 + i];
-                for (size_t j = 0; j < ns; ++j) L.coef[i][j] = mec::gf8_coef(coef[(r0 + i) * ns + j]);
+            if (!lay.tab) {
+                for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
+                for (int i = 0; i < rows; ++i) L.dst_off[i] = lay.dst_off[r0 + i];
             }
+            for (int i = 0; i < rows; ++i)
+                for (size_t j = 0; j < ns; ++j) L.coef[i][j] = mec::gf8_coef(coef[(r0 + i) * ns + j]);
             HIP_TRY(mec::launch_gf8(L, stream));
         } else {
             const Field &f = Field::get(int(c->w));
             mec::BmLaunch L{};
-            L.src = src;
-            L.dst = dst;
-            L.src_stripe_stride = sss;
-            L.dst_stripe_stride = dss;
+            L.src = lay.src;
+            L.dst = lay.dst;
+            L.src_stripe_stride = lay.sss;
+            L.dst_stripe_stride = lay.dss;
+            L.tab = lay.tab;
+            L.tab_stride = lay.tstride;
+            L.tab_dst = uint32_t(ns + r0);
             L.k = int(ns);
             L.rows = rows;
             L.w = int(c->w);
             L.packet = c->packet;
             L.n_stripes = n_stripes;
             L.accumulate = accumulate;
-            for (size_t j = 0; j < ns; ++j) L.src_off[j] = src_off[j];
-            for (int i = 0; i < rows; ++i) {
-                L.dst_off[i] = dst_off[r0 + i];
-                for (size_t j = 0; j < ns; ++j) {
-                    // block (i, j) of the bitmatrix: row l, column x = bit l of coef * 2^x
-                    unsigned e = coef[(r0 + i) * ns + j];
-                    uint8_t cols[8];
-                    for (uint32_t x = 0; x < c->w; ++x) {
-                        cols[x] = uint8_t(e);
-                        e = f.mul(e, 2 % f.size());
-                    }
-                    for (uint32_t l = 0; l < c->w; ++l) {
-                        uint8_t mb = 0;
-                        for (uint32_t x = 0; x < c->w; ++x) mb |= uint8_t((cols[x] >> l & 1) << x);
-                        L.mask[j][i * c->w + l] = mb;
-                    }
-                }
+            if (!lay.tab) {
+                for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
+                for (int i = 0; i < rows; ++i) L.dst_off[i] = lay.dst_off[r0 + i];
             }
+            for (int i = 0; i < rows; ++i)
+                for (size_t j = 0; j < ns; ++j)
+                    bit_block(f, coef[(r0 + i) * ns + j], c->w, &L.mask[j][i * c->w], 1);
             HIP_TRY(mec::launch_bm(L, stream));
         }
     }
     return MEC_OK;
+}
+
+int apply(mec_ctx *c, const uint8_t *src, int64_t sss, const std::vector<int64_t> &src_off, uint8_t *dst,
+          int64_t dss, const std::vector<int64_t> &dst_off, const Mat &coef, uint32_t n_stripes, bool accumulate,
+          hipStream_t stream) {
+    return apply(c, Layout::strided(src, sss, src_off, dst, dss, dst_off), coef, n_stripes, accumulate, stream);
 }
 
 int get_plan(mec_ctx *c, uint64_t present, std::shared_ptr<mec::LinearPlan> &out) {
@@ -235,21 +177,11 @@ void lane_release(mec_ctx *c, Lane *l) {
     c->lanes_free.push_back(l);
 }
 
-struct LaneHold {
-    mec_ctx *c;
-    Lane *l;
-    ~LaneHold() {
-        if (l) lane_release(c, l);
-    }
-};
 
-#define CHECK_CTX(c)                                                        \
-    do {                                                                    \
-        if (!(c)) return fail(MEC_EINVAL, "null context");                  \
-        if (!has_device(c)) return fail(MEC_ENODEV, "context has no device"); \
-    } while (0)
+}  // namespace core
+}  // namespace mec
 
-}  // namespace
+using namespace mec::core;
 
 extern "C" {
 
@@ -319,6 +251,7 @@ void mec_destroy(mec_ctx *c) {
     if (!c) return;
     if (has_device(c)) {
         DeviceGuard g(c->device);
+        batch_release(c);
         for (Lane *l : c->lanes_all) {
             (void)hipStreamSynchronize(l->stream);
             (void)hipFree(l->dev);
@@ -437,6 +370,7 @@ int mec_fill_random(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_off
 int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *parity) {
     CHECK_CTX(c);
     if (!data || !parity) return fail(MEC_EINVAL, "null pointer array");
+    if (coalescing(c)) return submit_encode(c, data, parity);
     DeviceGuard dg(c->device);
     int rc = MEC_OK;
     LaneHold h{c, lane_acquire(c, rc)};
@@ -465,6 +399,7 @@ int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *pari
 int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
     CHECK_CTX(c);
     if (!chunks) return fail(MEC_EINVAL, "null pointer array");
+    if (coalescing(c)) return submit_decode(c, chunks, present_mask);
     std::shared_ptr<mec::LinearPlan> plan;
     int rc = get_plan(c, present_mask, plan);
     if (rc != MEC_OK) return rc;
@@ -491,6 +426,7 @@ int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta
     CHECK_CTX(c);
     if (!delta || !parity) return fail(MEC_EINVAL, "null pointer");
     if (data_index >= c->k) return fail(MEC_EINVAL, "data_index %u >= k %u", data_index, c->k);
+    if (coalescing(c)) return submit_update(c, data_index, delta, parity);
     DeviceGuard dg(c->device);
     int rc = MEC_OK;
     LaneHold h{c, lane_acquire(c, rc)};

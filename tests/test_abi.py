@@ -113,6 +113,15 @@ def test_host_only_context_refuses_compute():
         with pytest.raises(MecError) as e:
             c.encode_host([np.zeros(4096, np.uint8)] * 4)
         assert e.value.code == _lib.MEC_ENODEV
+        a = np.zeros((6, 4096), np.uint8)
+        for call in (lambda: c.encode_batch([a[j].ctypes.data for j in range(4)],
+                                            [a[4 + i].ctypes.data for i in range(2)], mem="host"),
+                     lambda: c.encode_update_batch([0], [a[0].ctypes.data], [a[4].ctypes.data, 0], mem="host"),
+                     lambda: c.decode_batch([a[i].ctypes.data for i in range(6)], [0b111101], mem="host"),
+                     lambda: c.set_coalescing(8)):
+            with pytest.raises(MecError) as e:
+                call()
+            assert e.value.code == _lib.MEC_ENODEV
 
 
 def test_gf8_perm_decomposition_emulated():

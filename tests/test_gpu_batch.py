@@ -1,0 +1,314 @@
+"""GPU parity of the pointer-array batch ABI (mec_encode_batch,
+mec_decode_batch, mec_encode_update_batch) and the request coalescer,
+against the oracle.  Bit-exact.
+
+Chunks are scattered over a slab in random slot order, as server/ holds them
+(ChunkPool slots of 8 + chunkSize bytes, chunk_pool.cc:22-95, so chunk data
+is only 8-byte aligned; ChunkUtil::getData, chunk_util.hh:131-133), with
+Coding::zeros columns (NULL), unwanted parities (NULL) and, for decode, a
+different erasure pattern per stripe including none and more than m
+(recovery_worker.cc:210-296 batches stripes; worker.cc:49 decodes each).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import _lib  # noqa: E402
+
+DEV = "cuda:0"
+FAMS = ["rs", "cauchy", "isal_rs", "isal_cauchy"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    yield
+    torch.cuda.synchronize()
+
+
+class Slab:
+    """n_slots chunk slots of `slot` bytes; chunk data at +`hdr` (8 = the
+    reference's ChunkIdentifier header).  Device (torch) or host (numpy)."""
+
+    def __init__(self, n_slots, cs, hdr, device, seed):
+        self.cs, self.hdr, self.slot = cs, hdr, cs + hdr
+        nbytes = n_slots * self.slot
+        self.host = O.fill(nbytes, seed)
+        if device:
+            self.t = torch.from_numpy(self.host.copy()).to(DEV)
+            self.base = self.t.data_ptr()
+        else:
+            self.t = None
+            self.base = self.host.ctypes.data
+
+    def addr(self, i):
+        return self.base + i * self.slot + self.hdr
+
+    def chunk(self, i):
+        """Current contents of slot i's chunk (numpy copy)."""
+        if self.t is not None:
+            torch.cuda.synchronize()
+            return self.t[i * self.slot + self.hdr: i * self.slot + self.hdr + self.cs].cpu().numpy()
+        return self.host[i * self.slot + self.hdr: i * self.slot + self.hdr + self.cs].copy()
+
+    def snapshot(self):
+        if self.t is not None:
+            torch.cuda.synchronize()
+            return self.t.cpu().numpy()
+        return self.host.copy()
+
+
+def zeros(cs):
+    return np.zeros(cs, np.uint8)
+
+
+def chunk_of(snap, slab, i):
+    o = i * slab.slot + slab.hdr
+    return snap[o:o + slab.cs]
+
+
+# --------------------------------------------------------------------------- encode
+
+
+@pytest.mark.parametrize("mem", ["device", "host"])
+@pytest.mark.parametrize("fam", FAMS)
+@pytest.mark.parametrize("hdr", [8, 256])
+def test_encode_batch_scattered(fam, mem, hdr):
+    k, m, cs, n = 6, 3, 4096 if fam != "cauchy" else 4104, 40
+    if fam == "cauchy" and O.cauchy_getw(k, m, cs) < 0:
+        cs = 4096
+    rng = np.random.default_rng(7)
+    slots = rng.permutation(n * (k + m))
+    slab = Slab(n * (k + m), cs, hdr, mem == "device", 99)
+    before = slab.snapshot()
+    dptr, pptr, want = [], [], []
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        zero_cols = set(rng.choice(k, size=rng.integers(0, k + 1), replace=False).tolist()) if s % 3 == 0 else set()
+        wanted = [bool(rng.integers(0, 4)) for _ in range(m)] if s % 2 else [True] * m
+        dptr += [0 if j in zero_cols else slab.addr(row[j]) for j in range(k)]
+        pptr += [slab.addr(row[k + i]) if wanted[i] else 0 for i in range(m)]
+        data = [zeros(cs) if j in zero_cols else chunk_of(before, slab, row[j]).copy() for j in range(k)]
+        want.append((row, wanted, O.encode(fam, k, m, data, cs)))
+    c = Codec(fam, k, m, cs)
+    c.encode_batch(dptr, pptr, mem=mem)
+    after = slab.snapshot()
+    for s, (row, wanted, par) in enumerate(want):
+        for i in range(m):
+            got = chunk_of(after, slab, row[k + i])
+            if wanted[i]:
+                assert np.array_equal(got, par[i]), (fam, mem, s, i)
+            else:
+                assert np.array_equal(got, chunk_of(before, slab, row[k + i])), (fam, mem, s, i, "unwanted")
+        for j in range(k):  # sources untouched
+            assert np.array_equal(chunk_of(after, slab, row[j]), chunk_of(before, slab, row[j]))
+    # slot headers untouched
+    for i in range(n * (k + m)):
+        o = i * slab.slot
+        assert np.array_equal(after[o:o + hdr], before[o:o + hdr])
+
+
+def test_encode_batch_parity_mask_and_big_chunks_host():
+    """RS(10,4)@1MiB on host memory (chunks >= 256 KiB are DMA'd in place)."""
+    k, m, cs, n = 10, 4, 1 << 20, 3
+    c = Codec("rs", k, m, cs)
+    data = [O.fill(cs, 500 + i) for i in range(n * k)]
+    par = [np.full(cs, 0xA5, np.uint8) for _ in range(n * m)]
+    c.encode_batch([a.ctypes.data for a in data], [a.ctypes.data for a in par], parity_mask=0b1011, mem="host")
+    for s in range(n):
+        want = O.encode("rs", k, m, data[s * k:(s + 1) * k], cs)
+        for i in range(m):
+            if i == 2:
+                assert (par[s * m + i] == 0xA5).all()
+            else:
+                assert np.array_equal(par[s * m + i], want[i]), (s, i)
+
+
+# --------------------------------------------------------------------------- decode
+
+
+def random_patterns(rng, n, k, m):
+    pats = []
+    for s in range(n):
+        if s % 11 == 5:
+            e = m + 1  # too many: decode() == false, chunks untouched
+        elif s % 7 == 3:
+            e = 0
+        else:
+            e = int(rng.integers(1, m + 1))
+        pats.append(sorted(rng.choice(k + m, size=e, replace=False).tolist()))
+    return pats
+
+
+@pytest.mark.parametrize("mem", ["device", "host"])
+@pytest.mark.parametrize("fam", FAMS)
+def test_decode_batch_mixed_patterns(fam, mem):
+    k, m, cs, n = 6, 3, 2048, 48
+    rng = np.random.default_rng(11)
+    slots = rng.permutation(n * (k + m))
+    slab = Slab(n * (k + m), cs, 8, mem == "device", 1234)  # random (non-codeword) stripes
+    before = slab.snapshot()
+    pats = random_patterns(rng, n, k, m)
+    ptrs, masks = [], []
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        ptrs += [slab.addr(i) for i in row]
+        masks.append(sum(1 << i for i in range(k + m) if i not in pats[s]))
+    c = Codec(fam, k, m, cs)
+    res = c.decode_batch(ptrs, masks, mem=mem)
+    after = slab.snapshot()
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        chunks = [chunk_of(before, slab, i).copy() for i in row]
+        if len(pats[s]) > m:
+            assert res[s] == _lib.MEC_ETOOMANY, s
+            want = chunks
+        else:
+            assert res[s] == 0, (s, res[s])
+            if pats[s]:
+                assert O.decode(fam, k, m, chunks, pats[s], cs) == 0
+            want = chunks
+        for i in range(k + m):
+            assert np.array_equal(chunk_of(after, slab, row[i]), want[i]), (fam, mem, s, pats[s], i)
+    assert c.stats()["cached_plans"] == len({tuple(p) for p in pats if 0 < len(p) <= m})
+
+
+def test_decode_batch_roundtrip_baseline_shape():
+    """RS(10,4)@64KiB codewords, device, every stripe a different pattern of
+    4 erasures: decode restores the originals."""
+    k, m, cs, n = 10, 4, 65536, 64
+    c = Codec("rs", k, m, cs)
+    data = torch.empty(n, k, cs, dtype=torch.uint8, device=DEV)
+    fill_random(data, 4321)
+    par = torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)
+    c.encode(data, par)
+    stripe = torch.cat([data, par], dim=1).contiguous()
+    orig = stripe.clone()
+    rng = np.random.default_rng(5)
+    masks = []
+    for s in range(n):
+        pat = rng.choice(k + m, size=m, replace=False)
+        stripe[s, list(pat)] = 0
+        masks.append(sum(1 << i for i in range(k + m) if i not in pat))
+    base = stripe.data_ptr()
+    ptrs = [base + (s * (k + m) + i) * cs for s in range(n) for i in range(k + m)]
+    assert c.decode_batch(ptrs, masks) == [0] * n
+    torch.cuda.synchronize()
+    assert torch.equal(stripe, orig)
+
+
+# --------------------------------------------------------------------------- delta update
+
+
+@pytest.mark.parametrize("mem", ["device", "host"])
+@pytest.mark.parametrize("fam", FAMS)
+def test_update_batch(fam, mem):
+    """parity ^= A[:, j] * delta per stripe, mixed j: equals re-encoding the
+    updated data (parity_chunk_buffer.cc:340-415)."""
+    k, m, cs, n = 5, 3, 1024, 30
+    rng = np.random.default_rng(3)
+    data = [O.fill(k * cs, 70 + s).reshape(k, cs) for s in range(n)]
+    parity0 = [np.stack(O.encode(fam, k, m, list(d), cs)) for d in data]
+    deltas = [O.fill(cs, 900 + s) for s in range(n)]
+    js = [int(rng.integers(0, k)) for _ in range(n)]
+    wanted = [[bool(rng.integers(0, 3)) for _ in range(m)] for _ in range(n)]
+    c = Codec(fam, k, m, cs)
+    if mem == "device":
+        P = torch.from_numpy(np.stack(parity0)).to(DEV)
+        D = torch.from_numpy(np.stack(deltas)).to(DEV)
+        pb, db = P.data_ptr(), D.data_ptr()
+    else:
+        P = np.stack(parity0).copy()
+        D = np.stack(deltas)
+        pb, db = P.ctypes.data, D.ctypes.data
+    pptr = [pb + (s * m + i) * cs if wanted[s][i] else 0 for s in range(n) for i in range(m)]
+    dptr = [db + s * cs if s % 9 != 4 else 0 for s in range(n)]  # some all-zero deltas
+    c.encode_update_batch(js, dptr, pptr, mem=mem)
+    got = P.cpu().numpy() if mem == "device" else P
+    for s in range(n):
+        d2 = data[s].copy()
+        if s % 9 != 4:
+            d2[js[s]] ^= deltas[s]
+        want = O.encode(fam, k, m, list(d2), cs)
+        for i in range(m):
+            exp = want[i] if wanted[s][i] else parity0[s][i]
+            assert np.array_equal(got[s, i], exp), (fam, mem, s, i)
+
+
+# --------------------------------------------------------------------------- coalescer
+
+
+@pytest.mark.parametrize("fam", ["rs", "cauchy"])
+def test_coalesced_host_calls_from_threads(fam):
+    """Concurrent single-stripe mec_*_host calls (the server's worker threads
+    sharing one Coding, worker.cc:128-137) are batched and stay exact."""
+    k, m, cs = 8, 2, 4096
+    c = Codec(fam, k, m, cs)
+    c.set_coalescing(256)
+    n_threads, per = 12, 20
+    errors = []
+
+    def worker(t):
+        try:
+            for r in range(per):
+                seed = 10000 + t * 100 + r
+                data = [O.fill(cs, seed * 16 + j) for j in range(k)]
+                if r % 4 == 1:
+                    data[r % k] = None
+                got = c.encode_host(data)
+                want = O.encode(fam, k, m, [d if d is not None else zeros(cs) for d in data], cs)
+                for i in range(m):
+                    if not np.array_equal(got[i], want[i]):
+                        errors.append(("enc", t, r, i))
+                chunks = [d.copy() if d is not None else zeros(cs) for d in data] + [w.copy() for w in want]
+                orig = [x.copy() for x in chunks]
+                pat = [r % (k + m), (r * 3 + 1) % (k + m)] if r % 2 else [t % (k + m)]
+                for e in pat:
+                    chunks[e][:] = 0
+                c.decode_host(chunks, sum(1 << i for i in range(k + m) if i not in pat))
+                for i in range(k + m):
+                    if not np.array_equal(chunks[i], orig[i]):
+                        errors.append(("dec", t, r, i))
+                delta = O.fill(cs, seed + 7)
+                par = [w.copy() for w in want]
+                c.encode_update_host(r % k, delta, par)
+                d2 = [x.copy() for x in orig[:k]]
+                d2[r % k] ^= delta
+                want2 = O.encode(fam, k, m, d2, cs)
+                for i in range(m):
+                    if not np.array_equal(par[i], want2[i]):
+                        errors.append(("upd", t, r, i))
+        except Exception as exc:  # pragma: no cover - reported below
+            errors.append(("exc", t, repr(exc)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:10]
+    st = c.stats()
+    assert st["coalesced_requests"] == n_threads * per * 3
+    assert st["coalesced_batches"] <= st["coalesced_requests"]
+
+
+def test_batch_errors():
+    c = Codec("rs", 4, 2, 4096)
+    with pytest.raises(Exception):
+        c.encode_batch([0] * 4, [0] * 3)
+    with pytest.raises(_lib.MecError):
+        _lib.check(_lib.lib().mec_encode_batch(c._h, None, None, 1, 0, 0, None))
+    with pytest.raises(_lib.MecError):
+        _lib.check(_lib.lib().mec_encode_batch(c._h, None, None, 1, 0, 7, None))
+    # decode: NULL chunk pointer in a stripe that needs decoding -> EINVAL for that stripe
+    res = c.decode_batch([0] * 6, [0b111110])
+    assert res == [_lib.MEC_EINVAL]

@@ -1,0 +1,151 @@
+#!/usr/bin/env python3
+"""Throughput of the pointer-array batch ABI and the coalescer (one GPU).
+
+  device gather vs strided : same stripes, chunk pointers from a device table
+                             vs base + stride (RS(10,4)@1MiB, RS(8,2)@4KiB
+                             scattered over ChunkPool-like 8+cs slots)
+  decode_batch             : mixed erasure patterns per stripe
+  host batch               : mec_encode_batch on host memory (PCIe-inclusive)
+  coalescer                : T threads issuing single-stripe mec_encode_host
+                             calls, with and without coalescing
+
+Prints one JSON object per measurement.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from memec_amd import Codec, fill_random  # noqa: E402
+
+
+def timed(fn, reps, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps
+
+
+def gib(x):
+    return x / 2**30
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def device_gather(fam, k, m, cs, n, hdr, reps):
+    c = Codec(fam, k, m, cs)
+    slot = cs + hdr
+    slab = torch.empty(n * (k + m) * slot, dtype=torch.uint8, device="cuda")
+    fill_random(slab, 1)
+    perm = np.random.default_rng(0).permutation(n * (k + m))
+    base = slab.data_ptr()
+    rows = perm.reshape(n, k + m).astype(np.uint64) * np.uint64(slot) + np.uint64(base + hdr)
+    dptr = np.ascontiguousarray(rows[:, :k]).reshape(-1)
+    pptr = np.ascontiguousarray(rows[:, k:]).reshape(-1)
+    t_g = timed(lambda: c.encode_batch(dptr, pptr), reps)
+    data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
+    fill_random(data, 2)
+    par = torch.empty(n, m, cs, dtype=torch.uint8, device="cuda")
+    t_s = timed(lambda: c.encode(data, par), reps)
+    alg = n * (k + m) * cs
+    emit(test="device_gather_encode", family=fam, k=k, m=m, chunk=cs, stripes=n, slot_header=hdr,
+         gather_ms=round(t_g * 1e3, 4), strided_ms=round(t_s * 1e3, 4),
+         gather_GBps=round(alg / t_g / 1e9, 1), strided_GBps=round(alg / t_s / 1e9, 1),
+         note="gather time includes host-side grouping + pointer-table upload")
+    del slab, data, par
+
+
+def decode_mixed(fam, k, m, cs, n, n_patterns, reps):
+    c = Codec(fam, k, m, cs)
+    stripe = torch.empty(n, k + m, cs, dtype=torch.uint8, device="cuda")
+    fill_random(stripe, 3)
+    rng = np.random.default_rng(1)
+    pats = [sorted(rng.choice(k + m, size=m, replace=False).tolist()) for _ in range(n_patterns)]
+    masks = [sum(1 << i for i in range(k + m) if i not in pats[s % n_patterns]) for s in range(n)]
+    base = stripe.data_ptr()
+    ptrs = np.uint64(base) + np.arange(n * (k + m), dtype=np.uint64) * np.uint64(cs)
+    masks = np.asarray(masks, dtype=np.uint64)
+    t = timed(lambda: c.decode_batch(ptrs, masks), reps)
+    alg = n * (k + m) * cs
+    emit(test="decode_batch_mixed", family=fam, k=k, m=m, chunk=cs, stripes=n, patterns=n_patterns,
+         ms=round(t * 1e3, 4), GBps=round(alg / t / 1e9, 1), data_GiBps=round(gib(n * k * cs) / t, 1))
+    del stripe
+
+
+def host_batch(fam, k, m, cs, n, reps):
+    c = Codec(fam, k, m, cs)
+    slot = cs + 8
+    slab = np.random.default_rng(0).integers(0, 256, n * (k + m) * slot, dtype=np.uint8)
+    base = slab.ctypes.data
+    rows = np.arange(n * (k + m), dtype=np.uint64).reshape(n, k + m) * np.uint64(slot) + np.uint64(base + 8)
+    dptr = np.ascontiguousarray(rows[:, :k]).reshape(-1)
+    pptr = np.ascontiguousarray(rows[:, k:]).reshape(-1)
+    t = timed(lambda: c.encode_batch(dptr, pptr, mem="host"), reps, warm=1)
+    emit(test="host_encode_batch", family=fam, k=k, m=m, chunk=cs, stripes=n, memory="pageable",
+         ms=round(t * 1e3, 3), data_GiBps=round(gib(n * k * cs) / t, 2))
+
+
+def coalescer(fam, k, m, cs, threads, per_thread, max_batch):
+    c = Codec(fam, k, m, cs)
+    if max_batch:
+        c.set_coalescing(max_batch)
+    bufs = [[np.random.default_rng(t * 100 + j).integers(0, 256, cs, dtype=np.uint8) for j in range(k)]
+            for t in range(threads)]
+
+    def worker(t):
+        for _ in range(per_thread):
+            c.encode_host(bufs[t])
+
+    def run():
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+
+    run()  # warm
+    t0 = time.perf_counter()
+    run()
+    dt = time.perf_counter() - t0
+    st = c.stats()
+    n = threads * per_thread
+    emit(test="coalescer_encode_host", family=fam, k=k, m=m, chunk=cs, threads=threads, calls=n,
+         max_batch=max_batch, calls_per_s=round(n / dt, 1), data_GiBps=round(gib(n * k * cs) / dt, 3),
+         mean_batch=round(st["coalesced_requests"] / st["coalesced_batches"], 2) if st["coalesced_batches"] else 1)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    a = ap.parse_args()
+    reps = 3 if a.quick else 10
+    torch.cuda.set_device(0)
+    device_gather("rs", 10, 4, 1 << 20, 1024, 8, reps)
+    device_gather("rs", 10, 4, 1 << 20, 1024, 256, reps)
+    device_gather("rs", 8, 2, 4096, 65536, 8, reps)
+    device_gather("rs", 8, 2, 4096, 65536, 256, reps)
+    device_gather("cauchy", 12, 4, 65536, 4096, 8, reps)
+    for npat in (1, 4, 14, 64):
+        decode_mixed("rs", 10, 4, 65536, 4096, npat, reps)
+    decode_mixed("cauchy", 12, 4, 65536, 4096, 4, reps)
+    host_batch("rs", 8, 2, 4096, 16384, reps)
+    host_batch("rs", 10, 4, 1 << 20, 64, reps)
+    for mb in (0, 256):
+        coalescer("rs", 8, 2, 4096, 16, 200, mb)
+
+
+if __name__ == "__main__":
+    main()

@@ -4,6 +4,7 @@
 #   tests   pytest -m gpu          smoke   __graft_entry__.smoke()
 #   bench   bench.py (default)     prof    rocprofv3 --kernel-trace --stats of bench
 #   benchall  bench.py for every config (no cpu baseline)
+#   batch   tools/bench_batch.py (pointer batches, coalescer)
 #   pmc     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench
 set -u
 cd "$(dirname "$0")/.."
@@ -35,6 +36,7 @@ for step in "$@"; do
             for c in rs_enc rs_dec rs_dec_mixed rs8_small crs_enc crs_dec rs42; do
                 run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --steps 10
             done ;;
+        batch) run bench_batch 600 python tools/bench_batch.py ;;
         e2e) run bench_e2e 400 python bench.py --e2e --no-cpu-baseline --steps 5 ;;
         prof)
             for c in ${PROF_CONFIGS:-rs_enc}; do
