@@ -32,6 +32,7 @@ struct Group {
     std::vector<uint64_t> ptrs;  // n rows of [ns sources | nd outputs]
     std::vector<int32_t> owner;  // per stripe: index of the request / stripe it came from
     std::shared_ptr<LinearPlan> plan;  // decode groups: survivor / output chunk indices
+    std::vector<uint32_t> cols, rows;  // encode / update groups: source columns, output rows
 };
 
 struct GroupSet {
@@ -68,14 +69,15 @@ void add_encode(mec_ctx *c, GroupSet &G, const uint8_t *const *data, uint8_t *co
     if (!dm) return;
     bool fresh;
     Group &g = G.get(uint64_t(sm) | uint64_t(dm) << 32, fresh);
-    const std::vector<uint32_t> cols = bits_of(sm, c->k), rows = bits_of(dm, c->m);
     if (fresh) {
-        g.coef = encode_rows(c, rows, cols);
-        g.ns = uint32_t(cols.size());
-        g.nd = uint32_t(rows.size());
+        g.cols = bits_of(sm, c->k);
+        g.rows = bits_of(dm, c->m);
+        g.coef = encode_rows(c, g.rows, g.cols);
+        g.ns = uint32_t(g.cols.size());
+        g.nd = uint32_t(g.rows.size());
     }
-    for (uint32_t j : cols) g.ptrs.push_back(uint64_t(uintptr_t(data[j])));
-    for (uint32_t i : rows) g.ptrs.push_back(uint64_t(uintptr_t(parity[i])));
+    for (uint32_t j : g.cols) g.ptrs.push_back(uint64_t(uintptr_t(data[j])));
+    for (uint32_t i : g.rows) g.ptrs.push_back(uint64_t(uintptr_t(parity[i])));
     g.owner.push_back(owner);
     ++g.n;
 }
@@ -89,15 +91,15 @@ void add_update(mec_ctx *c, GroupSet &G, uint32_t j, const uint8_t *delta, uint8
     if (!dm) return;
     bool fresh;
     Group &g = G.get(uint64_t(j) | uint64_t(dm) << 8, fresh);
-    const std::vector<uint32_t> rows = bits_of(dm, c->m);
     if (fresh) {
-        g.coef = encode_rows(c, rows, {j});
+        g.rows = bits_of(dm, c->m);
+        g.coef = encode_rows(c, g.rows, {j});
         g.ns = 1;
-        g.nd = uint32_t(rows.size());
+        g.nd = uint32_t(g.rows.size());
         g.accumulate = true;
     }
     g.ptrs.push_back(uint64_t(uintptr_t(delta)));
-    for (uint32_t i : rows) g.ptrs.push_back(uint64_t(uintptr_t(parity[i])));
+    for (uint32_t i : g.rows) g.ptrs.push_back(uint64_t(uintptr_t(parity[i])));
     g.owner.push_back(owner);
     ++g.n;
 }
@@ -134,29 +136,100 @@ int add_decode(mec_ctx *c, GroupSet &G, uint8_t *const *chunks, uint64_t present
 }
 
 // ---------------------------------------------------------------------------
-// device-resident execution: one table upload, one gather launch per group
+// device-resident execution: the caller's pointer rows are uploaded as they
+// are, every stripe carries a descriptor index, and each group of <= 4
+// output rows is ONE gathered launch whatever the mix of patterns
 // ---------------------------------------------------------------------------
-int run_device(mec_ctx *c, std::vector<Group> &gs, hipStream_t st) {
-    size_t total = 0;
-    for (Group &g : gs) {
-        if (!g.n || !g.nd) continue;
-        if (!g.ns) {  // every source is the zeros sentinel: outputs are zero
-            if (g.accumulate) continue;
-            for (uint32_t s = 0; s < g.n; ++s)
-                for (uint32_t r = 0; r < g.nd; ++r)
-                    HIP_TRY(hipMemsetAsync(reinterpret_cast<void *>(g.ptrs[size_t(s) * g.nd + r]), 0, c->cs, st));
-            continue;
-        }
-        total += g.ptrs.size();
+
+// The linear maps of a device batch: map p reads sources ssel[p] (entries of
+// the stripe's source row) and writes outputs dsel[p] with coef[p]
+// (dsel.size() x K over GF(2^w)).
+struct MapSet {
+    uint32_t K = 0;
+    bool accumulate = false;
+    std::vector<std::vector<uint8_t>> ssel, dsel;
+    std::vector<Mat> coef;
+    size_t rows() const {
+        size_t r = 0;
+        for (const auto &d : dsel) r = std::max(r, d.size());
+        return r;
     }
-    if (!total) return MEC_OK;
+    uint32_t add(std::vector<uint8_t> s, std::vector<uint8_t> d, Mat c) {
+        ssel.push_back(std::move(s));
+        dsel.push_back(std::move(d));
+        coef.push_back(std::move(c));
+        return uint32_t(ssel.size() - 1);
+    }
+};
+
+// Descriptor blobs [row group][map] (layout in kernels.hpp).
+size_t build_descs(const mec_ctx *c, const MapSet &M, std::vector<uint32_t> &out, uint32_t &desc_dw) {
+    const size_t groups = (M.rows() + kMaxRows - 1) / kMaxRows, nm = M.ssel.size();
+    const uint32_t K = M.K;
+    desc_dw = c->byte_wise() ? uint32_t(kGf8DescHead + kMaxRows * K * 8) : uint32_t(kBmDescHead + kMaxSrc * c->w);
+    out.assign(groups * nm * desc_dw, 0);
+    auto put_byte = [](uint32_t *w, size_t idx, uint8_t v) { w[idx / 4] |= uint32_t(v) << (8 * (idx % 4)); };
+    for (size_t g = 0; g < groups; ++g)
+        for (size_t q = 0; q < nm; ++q) {
+            uint32_t *D = out.data() + (g * nm + q) * desc_dw;
+            const size_t nd = M.dsel[q].size();
+            const uint32_t sel_dw = c->byte_wise() ? 8 : 0, dsel_dw = c->byte_wise() ? 16 : 8;
+            for (uint32_t j = 0; j < K; ++j) put_byte(D + sel_dw, j, M.ssel[q][j]);
+            for (int i = 0; i < kMaxRows; ++i) {
+                const size_t r = g * kMaxRows + i;
+                put_byte(D + dsel_dw, i, r < nd ? M.dsel[q][r] : kNoRow);
+            }
+            if (c->byte_wise()) {
+                for (int i = 0; i < kMaxRows; ++i) {
+                    const size_t r = g * kMaxRows + i;
+                    for (uint32_t j = 0; j < K; ++j) {
+                        const uint8_t e = r < nd ? M.coef[q][r * K + j] : 0;
+                        const uint32_t b = uint32_t(i) * K + j;
+                        const Gf8Coef cf = gf8_coef(e);
+                        uint32_t *t = D + kGf8DescHead + b * 8;
+                        t[0] = cf.t0;
+                        t[1] = cf.t1;
+                        t[2] = cf.u0;
+                        t[3] = cf.u1;
+                        t[4] = cf.v;
+                        if (e == 0) D[4 + b / 32] |= 1u << (b % 32);
+                        if (e == 1) D[b / 32] |= 1u << (b % 32);
+                    }
+                }
+            } else {
+                const Field &f = Field::get(int(c->w));
+                for (int i = 0; i < kMaxRows; ++i) {
+                    const size_t r = g * kMaxRows + i;
+                    if (r >= nd) continue;
+                    for (uint32_t j = 0; j < K; ++j) {
+                        uint8_t mask[8];
+                        bit_block(f, M.coef[q][r * K + j], c->w, mask, 1);
+                        for (uint32_t l = 0; l < c->w; ++l)
+                            put_byte(D + kBmDescHead + j * c->w, i * c->w + l, mask[l]);
+                    }
+                }
+            }
+        }
+    return groups;
+}
+
+// Pinned + device staging of one call's tables, reused round-robin.
+int table_upload(mec_ctx *c, const std::vector<std::pair<const void *, size_t>> &parts, TableSlot *&slot,
+                 std::vector<size_t> &offs, hipStream_t st) {
+    size_t total = 0;
+    offs.clear();
+    for (const auto &pr : parts) {
+        offs.push_back(total);
+        total += (pr.second + 255) & ~size_t(255);
+    }
     uint32_t idx;
     {
         std::lock_guard<std::mutex> lk(c->tab_mu);
         idx = c->tab_next++ % kTableSlots;
     }
     TableSlot &t = c->tabs[idx];
-    std::lock_guard<std::mutex> lk(t.mu);
+    t.mu.lock();
+    slot = &t;
     if (t.pending) {
         HIP_TRY(hipEventSynchronize(t.done));
         t.pending = false;
@@ -168,30 +241,74 @@ int run_device(mec_ctx *c, std::vector<Group> &gs, hipStream_t st) {
         t.host = nullptr;
         t.dev = nullptr;
         t.cap = 0;
-        const size_t cap = std::max<size_t>(total, 4096);
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.host), cap * sizeof(uint64_t), hipHostMallocDefault));
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&t.dev), cap * sizeof(uint64_t)));
+        const size_t cap = std::max<size_t>(total, size_t(1) << 20);
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.host), cap, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&t.dev), cap));
         t.cap = cap;
     }
-    size_t off = 0;
-    for (Group &g : gs) {
-        if (!g.n || !g.nd || !g.ns) continue;
-        std::memcpy(t.host + off, g.ptrs.data(), g.ptrs.size() * sizeof(uint64_t));
-        off += g.ptrs.size();
+    uint8_t *h = reinterpret_cast<uint8_t *>(t.host);
+    for (size_t i = 0; i < parts.size(); ++i)
+        if (parts[i].second) std::memcpy(h + offs[i], parts[i].first, parts[i].second);
+    HIP_TRY(hipMemcpyAsync(t.dev, t.host, total, hipMemcpyHostToDevice, st));
+    return MEC_OK;
+}
+
+struct SlotHold {
+    TableSlot *t = nullptr;
+    hipStream_t st = nullptr;
+    ~SlotHold() {
+        if (!t) return;
+        // recorded even after a failed launch so the slot is never reused early
+        if (hipEventRecord(t->done, st) == hipSuccess) t->pending = true;
+        t->mu.unlock();
     }
-    HIP_TRY(hipMemcpyAsync(t.dev, t.host, total * sizeof(uint64_t), hipMemcpyHostToDevice, st));
-    off = 0;
-    int rc = MEC_OK;
-    for (Group &g : gs) {
-        if (!g.n || !g.nd || !g.ns) continue;
-        rc = apply(c, Layout::gather(t.dev + off, g.ns, g.nd), g.coef, g.n, g.accumulate, st);
-        if (rc != MEC_OK) break;
-        off += g.ptrs.size();
+};
+
+// stab / dtab: host arrays of n rows of device chunk pointers; pat: per-stripe
+// map index (nullptr = map 0).
+int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, const void *dtab, uint32_t dstride,
+               const uint16_t *pat, uint32_t n, hipStream_t st) {
+    if (M.ssel.empty() || M.rows() == 0 || n == 0) return MEC_OK;
+    std::vector<uint32_t> descs;
+    uint32_t desc_dw = 0;
+    const size_t groups = build_descs(c, M, descs, desc_dw);
+    const bool same = stab == dtab && sstride == dstride;
+    std::vector<std::pair<const void *, size_t>> parts = {
+        {stab, size_t(n) * sstride * 8},
+        {same ? nullptr : dtab, same ? 0 : size_t(n) * dstride * 8},
+        {pat, pat ? size_t(n) * 2 : 0},
+        {descs.data(), descs.size() * sizeof(uint32_t)}};
+    SlotHold hold;
+    hold.st = st;
+    std::vector<size_t> offs;
+    int rc = table_upload(c, parts, hold.t, offs, st);
+    if (rc != MEC_OK) return rc;
+    uint8_t *dev = reinterpret_cast<uint8_t *>(hold.t->dev);
+    GatherLaunch L{};
+    L.stab = reinterpret_cast<const uint64_t *>(dev + offs[0]);
+    L.dtab = reinterpret_cast<const uint64_t *>(dev + offs[same ? 0 : 1]);
+    L.sstride = sstride;
+    L.dstride = dstride;
+    L.pat = pat ? reinterpret_cast<const uint16_t *>(dev + offs[2]) : nullptr;
+    L.n_stripes = n;
+    L.k = int(M.K);
+    L.accumulate = M.accumulate;
+    const size_t rows = M.rows(), nm = M.ssel.size();
+    for (size_t g = 0; g < groups; ++g) {
+        L.rows = int(std::min<size_t>(kMaxRows, rows - g * kMaxRows));
+        L.desc = dev + offs[3] + g * nm * desc_dw * sizeof(uint32_t);
+        L.desc_dw = desc_dw;
+        if (c->byte_wise()) {
+            L.w = 0;
+            L.len = c->cs;
+            HIP_TRY(launch_gf8_gather(L, st));
+        } else {
+            L.w = int(c->w);
+            L.len = c->packet;
+            HIP_TRY(launch_bm_gather(L, st));
+        }
     }
-    // recorded even after a failed launch so the slot is never reused early
-    HIP_TRY(hipEventRecord(t.done, st));
-    t.pending = true;
-    return rc;
+    return MEC_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -359,11 +476,6 @@ int run_host(mec_ctx *c, std::vector<Group> &gs) {
     return rc;
 }
 
-int run(mec_ctx *c, std::vector<Group> &gs, int kind, hipStream_t st) {
-    if (kind == MEC_MEM_DEVICE) return run_device(c, gs, st);
-    return run_host(c, gs);
-}
-
 // ---------------------------------------------------------------------------
 // coalescer: concurrent single-stripe host calls become one batch
 // ---------------------------------------------------------------------------
@@ -487,6 +599,7 @@ void batch_release(mec_ctx *c) {
 }  // namespace core
 }  // namespace mec
 
+using namespace mec;
 using namespace mec::core;
 
 extern "C" {
@@ -498,11 +611,21 @@ int mec_encode_batch(mec_ctx *c, const uint8_t *const *data, uint8_t *const *par
     if (n_stripes == 0) return MEC_OK;
     if (!data || !parity) return fail(MEC_EINVAL, "null pointer array");
     const uint32_t pm = parity_mask ? parity_mask : full_mask32(c->m);
+    DeviceGuard dg(c->device);
+    if (mem_kind == MEC_MEM_DEVICE) {
+        // one map: all k columns (NULL sources read as zero), the masked rows
+        // (NULL outputs are skipped in the kernel)
+        MapSet M;
+        M.K = c->k;
+        std::vector<uint32_t> rows = bits_of(pm, c->m), cols = bits_of(full_mask32(c->k), c->k);
+        std::vector<uint8_t> ss(cols.begin(), cols.end()), ds(rows.begin(), rows.end());
+        M.add(ss, ds, encode_rows(c, rows, cols));
+        return run_gather(c, M, data, c->k, parity, c->m, nullptr, n_stripes, hipStream_t(stream));
+    }
     GroupSet G;
     for (uint32_t s = 0; s < n_stripes; ++s)
         add_encode(c, G, data + size_t(s) * c->k, parity + size_t(s) * c->m, pm, int32_t(s));
-    DeviceGuard dg(c->device);
-    return run(c, G.groups, mem_kind, hipStream_t(stream));
+    return run_host(c, G.groups);
 }
 
 int mec_decode_batch(mec_ctx *c, uint8_t *const *chunks, const uint64_t *present_masks, uint32_t n_stripes,
@@ -511,20 +634,68 @@ int mec_decode_batch(mec_ctx *c, uint8_t *const *chunks, const uint64_t *present
     if (mem_kind != MEC_MEM_DEVICE && mem_kind != MEC_MEM_HOST) return fail(MEC_EINVAL, "bad mem_kind %d", mem_kind);
     if (n_stripes == 0) return MEC_OK;
     if (!chunks || !present_masks) return fail(MEC_EINVAL, "null pointer array");
-    GroupSet G;
     int first = MEC_OK;
     std::string first_err;
     const uint32_t n = c->k + c->m;
-    for (uint32_t s = 0; s < n_stripes; ++s) {
-        const int rc = add_decode(c, G, chunks + size_t(s) * n, present_masks[s], int32_t(s));
+    const uint64_t full = (uint64_t(1) << n) - 1;
+    auto note = [&](uint32_t s, int rc) {
         if (results) results[s] = rc;
         if (rc != MEC_OK && first == MEC_OK) {
             first = rc;
             first_err = "stripe " + std::to_string(s) + ": " + g_err;
         }
-    }
+    };
     DeviceGuard dg(c->device);
-    const int rc = run(c, G.groups, mem_kind, hipStream_t(stream));
+    int rc = MEC_OK;
+    if (mem_kind == MEC_MEM_DEVICE) {
+        MapSet M;
+        M.K = c->k;
+        std::vector<uint16_t> pat(n_stripes, kSkipStripe);
+        std::unordered_map<uint64_t, uint16_t> ids;
+        uint64_t last_mask = ~uint64_t(0);
+        uint16_t last_id = kSkipStripe;
+        for (uint32_t s = 0; s < n_stripes; ++s) {
+            const uint64_t present = present_masks[s] & full;
+            uint8_t *const *row = chunks + size_t(s) * n;
+            int src = MEC_OK;
+            const uint32_t failed = uint32_t(__builtin_popcountll(~present & full));
+            if (failed > c->m) {
+                src = fail(MEC_ETOOMANY, "Too many failure to recover (%u>%u)", failed, c->m);
+            } else if (failed > 0) {
+                for (uint32_t i = 0; i < n && src == MEC_OK; ++i)
+                    if (!row[i]) src = fail(MEC_EINVAL, "chunk %u pointer is NULL", i);
+                if (src == MEC_OK) {
+                    if (present != last_mask) {
+                        auto it = ids.find(present);
+                        if (it == ids.end()) {
+                            std::shared_ptr<LinearPlan> plan;
+                            src = get_plan(c, present, plan);
+                            if (src == MEC_OK) {
+                                if (M.ssel.size() >= kSkipStripe) {
+                                    src = fail(MEC_EINVAL, "too many distinct erasure patterns in one batch");
+                                } else {
+                                    std::vector<uint8_t> ss(plan->src.begin(), plan->src.end());
+                                    std::vector<uint8_t> ds(plan->dst.begin(), plan->dst.end());
+                                    it = ids.emplace(present, uint16_t(M.add(ss, ds, plan->coef))).first;
+                                }
+                            }
+                        }
+                        if (src == MEC_OK) {
+                            last_mask = present;
+                            last_id = it->second;
+                        }
+                    }
+                    if (src == MEC_OK) pat[s] = last_id;
+                }
+            }
+            note(s, src);
+        }
+        rc = run_gather(c, M, chunks, n, chunks, n, pat.data(), n_stripes, hipStream_t(stream));
+    } else {
+        GroupSet G;
+        for (uint32_t s = 0; s < n_stripes; ++s) note(s, add_decode(c, G, chunks + size_t(s) * n, present_masks[s], int32_t(s)));
+        rc = run_host(c, G.groups);
+    }
     if (rc != MEC_OK) {
         if (results)
             for (uint32_t s = 0; s < n_stripes; ++s)
@@ -542,15 +713,29 @@ int mec_encode_update_batch(mec_ctx *c, const uint32_t *data_index, const uint8_
     if (mem_kind != MEC_MEM_DEVICE && mem_kind != MEC_MEM_HOST) return fail(MEC_EINVAL, "bad mem_kind %d", mem_kind);
     if (n_stripes == 0) return MEC_OK;
     if (!data_index || !delta || !parity) return fail(MEC_EINVAL, "null pointer array");
+    for (uint32_t s = 0; s < n_stripes; ++s)
+        if (data_index[s] >= c->k) return fail(MEC_EINVAL, "stripe %u: data_index %u >= k %u", s, data_index[s], c->k);
     const uint32_t pm = parity_mask ? parity_mask : full_mask32(c->m);
+    DeviceGuard dg(c->device);
+    if (mem_kind == MEC_MEM_DEVICE) {
+        // map j = delta column j (one source, the masked rows); the stripe's
+        // data_index picks it, a NULL delta skips the stripe
+        MapSet M;
+        M.K = 1;
+        M.accumulate = true;
+        const std::vector<uint32_t> rows = bits_of(pm, c->m);
+        const std::vector<uint8_t> ds(rows.begin(), rows.end());
+        for (uint32_t j = 0; j < c->k; ++j) M.add({0}, ds, encode_rows(c, rows, {j}));
+        std::vector<uint16_t> pat(n_stripes);
+        for (uint32_t s = 0; s < n_stripes; ++s) pat[s] = delta[s] ? uint16_t(data_index[s]) : kSkipStripe;
+        return run_gather(c, M, delta, 1, parity, c->m, pat.data(), n_stripes, hipStream_t(stream));
+    }
     GroupSet G;
     for (uint32_t s = 0; s < n_stripes; ++s) {
-        if (data_index[s] >= c->k) return fail(MEC_EINVAL, "stripe %u: data_index %u >= k %u", s, data_index[s], c->k);
         if (!delta[s]) continue;  // an all-zero delta changes nothing
         add_update(c, G, data_index[s], delta[s], parity + size_t(s) * c->m, pm, int32_t(s));
     }
-    DeviceGuard dg(c->device);
-    return run(c, G.groups, mem_kind, hipStream_t(stream));
+    return run_host(c, G.groups);
 }
 
 int mec_set_coalescing(mec_ctx *c, uint32_t max_batch) {

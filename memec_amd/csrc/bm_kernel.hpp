@@ -45,8 +45,6 @@ struct BmParams {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
-    const uint64_t *tab;  // gather mode: per stripe [k sources | dsts] chunk pointers
-    uint32_t tstride, tdst;
     uint64_t packet;
     uint32_t units, tiles, k, accumulate;
     int64_t src_off[kMaxSrc];
@@ -59,7 +57,7 @@ constexpr int bm_vw() {
     return W <= 4 ? 4 : 2;
 }
 
-template <int W, int R, bool G>
+template <int W, int R>
 __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
     constexpr int VW = bm_vw<W>();
     constexpr int ROWS = R * W;
@@ -68,27 +66,8 @@ __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
     const uint32_t u = (blockIdx.x - stripe * p.tiles) * kThreads + threadIdx.x;
     if (u >= p.units) return;
     const uint64_t off = uint64_t(u) * (4 * VW);
-    const uint8_t *sb = nullptr;
-    uint8_t *db = nullptr;
-    const uint64_t *row = nullptr;
-    if constexpr (G) {
-        row = p.tab + uint64_t(stripe) * p.tstride;
-    } else {
-        sb = p.src + int64_t(stripe) * p.sss + off;
-        db = p.dst + int64_t(stripe) * p.dss + off;
-    }
-    auto src = [&](uint32_t j) -> const uint8_t * {
-        if constexpr (G)
-            return reinterpret_cast<const uint8_t *>(row[j]) + off;
-        else
-            return sb + p.src_off[j];
-    };
-    auto dp = [&](int i) -> uint8_t * {
-        if constexpr (G)
-            return reinterpret_cast<uint8_t *>(row[p.tdst + i]) + off;
-        else
-            return db + p.dst_off[i];
-    };
+    const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
+    uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
 
     vec acc[ROWS];
     if (p.accumulate) {
@@ -96,22 +75,18 @@ __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
         for (int i = 0; i < R; ++i)
 #pragma unroll
             for (int l = 0; l < W; ++l)
-                acc[i * W + l] = *reinterpret_cast<const vec *>(dp(i) + uint64_t(l) * p.packet);
+                acc[i * W + l] = *reinterpret_cast<const vec *>(db + p.dst_off[i] + uint64_t(l) * p.packet);
     } else {
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) acc[r] = vec(0);
     }
     vec d[W], nx[W];
-    {
-        const uint8_t *s0 = src(0);
 #pragma unroll
-        for (int x = 0; x < W; ++x) d[x] = ld_nt<vec>(s0 + uint64_t(x) * p.packet);
-    }
+    for (int x = 0; x < W; ++x) d[x] = ld_nt<vec>(sb + p.src_off[0] + uint64_t(x) * p.packet);
     for (uint32_t j = 0; j < p.k; ++j) {
         if (j + 1 < p.k) {
-            const uint8_t *s1 = src(j + 1);
 #pragma unroll
-            for (int x = 0; x < W; ++x) nx[x] = ld_nt<vec>(s1 + uint64_t(x) * p.packet);
+            for (int x = 0; x < W; ++x) nx[x] = ld_nt<vec>(sb + p.src_off[j + 1] + uint64_t(x) * p.packet);
         }
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
@@ -130,7 +105,7 @@ __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
 #pragma unroll
     for (int i = 0; i < R; ++i)
 #pragma unroll
-        for (int l = 0; l < W; ++l) st_nt<vec>(dp(i) + uint64_t(l) * p.packet, acc[i * W + l]);
+        for (int l = 0; l < W; ++l) st_nt<vec>(db + p.dst_off[i] + uint64_t(l) * p.packet, acc[i * W + l]);
 }
 
 hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream);
@@ -143,8 +118,6 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     p.dss = L.dst_stripe_stride;
     p.packet = L.packet;
     p.k = uint32_t(L.k);
-    p.tstride = L.tab_stride;
-    p.tdst = L.tab_dst;
     const Geometry g = geometry(L.packet / UB);
     p.units = g.units;
     p.tiles = g.tiles;
@@ -156,17 +129,9 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     if (g.units > 0) {
         for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-            if (L.tab) {
-                p.src = nullptr;
-                p.dst = nullptr;
-                p.tab = L.tab + uint64_t(s0) * L.tab_stride;
-                hipLaunchKernelGGL((bm_kernel<W, R, true>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-            } else {
-                p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-                p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-                p.tab = nullptr;
-                hipLaunchKernelGGL((bm_kernel<W, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-            }
+            p.src = L.src + int64_t(s0) * L.src_stripe_stride;
+            p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+            hipLaunchKernelGGL((bm_kernel<W, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

@@ -143,15 +143,13 @@ inline bool has_device(const mec_ctx *c) { return c->device >= 0; }
         if (!has_device(c)) return fail(MEC_ENODEV, "context has no device"); \
     } while (0)
 
-// Where a launch finds its chunks: strided (base + stripe * stride +
-// offset) or gathered from a device table of per-stripe chunk pointers.
+// Strided chunk addressing of a launch: source j of stripe s at
+// src + s * sss + src_off[j], output r at dst + s * dss + dst_off[r].
 struct Layout {
     const uint8_t *src = nullptr;
     uint8_t *dst = nullptr;
     int64_t sss = 0, dss = 0;
-    std::vector<int64_t> src_off, dst_off;  // strided: one per source / output
-    const uint64_t *tab = nullptr;          // gather: rows [ns sources | nd outputs]
-    uint32_t tstride = 0;
+    std::vector<int64_t> src_off, dst_off;
     size_t ns = 0, nd = 0;
 
     static Layout strided(const uint8_t *src, int64_t sss, std::vector<int64_t> so, uint8_t *dst, int64_t dss,
@@ -165,14 +163,6 @@ struct Layout {
         l.nd = dof.size();
         l.src_off = std::move(so);
         l.dst_off = std::move(dof);
-        return l;
-    }
-    static Layout gather(const uint64_t *tab, size_t ns, size_t nd) {
-        Layout l;
-        l.tab = tab;
-        l.tstride = uint32_t(ns + nd);
-        l.ns = ns;
-        l.nd = nd;
         return l;
     }
 };

@@ -1,0 +1,296 @@
+// gather_kernel.hpp — descriptor-driven gathered variants of the gf8 and
+// bitmatrix kernels, for the pointer-array batches (mec_encode_batch,
+// mec_decode_batch, mec_encode_update_batch).
+//
+// A block serves one (stripe, 256-unit tile) as in the strided kernels.  It
+// finds its chunks through two device tables of chunk pointers (the
+// caller's Chunk* rows, uploaded as they are) and its linear map through a
+// descriptor: the stripe's erasure pattern (decode) or delta column
+// (update) selects one, so every pattern in a batch shares one launch.
+// A block's table entries are fetched once, cooperatively, into LDS and
+// read back as wave-uniform SGPR values; each chunk is then a buffer
+// resource (32-bit offsets, range-checked).  A NULL source pointer is an
+// all-zero chunk (Coding::zeros, coding.cc:14-16): its resource has zero
+// records, so it is not read; a NULL output is not written, the same way.
+#pragma once
+
+#include "bm_kernel.hpp"
+#include "gf8_kernel.hpp"
+#include "stream_common.hpp"
+
+namespace mec {
+namespace detail {
+
+struct GatherParams {
+    const uint64_t *stab;
+    const uint64_t *dtab;
+    const uint32_t *desc;  // descriptor blobs (layout in kernels.hpp), desc_dw dwords apart
+    const uint16_t *pat;
+    uint64_t packet;  // bitmatrix packet bytes
+    uint32_t chunk;   // bytes per chunk (buffer range)
+    uint32_t desc_dw;
+    uint32_t sstride, dstride;
+    uint32_t s0, units, tiles, k, accumulate;
+};
+
+__device__ __forceinline__ uint32_t gather_desc(const GatherParams &p, uint32_t s) {
+    return p.pat ? uint32_t(p.pat[s]) : 0u;
+}
+
+// Uniform 64-bit / 32-bit values read back from LDS into SGPRs.
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+    return uint64_t(hi) << 32 | lo;
+}
+__device__ __forceinline__ uint32_t uniform32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// One chunk as a buffer resource: a NULL chunk gets zero records, so its
+// loads return 0 and its stores are dropped by the range check — no
+// branches around the memory operations.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(uint64_t a, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(a), 0, a ? int(bytes) : 0, 0x00020000);
+}
+constexpr int kAuxNT = 2;  // non-temporal (streamed once)
+template <typename V>
+__device__ __forceinline__ V buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt);
+template <>
+__device__ __forceinline__ u32x4 buf_ld<u32x4>(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
+    return nt ? __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxNT) : __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+template <>
+__device__ __forceinline__ u32x2 buf_ld<u32x2>(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
+    return nt ? __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxNT) : __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_st(u32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxNT);
+}
+__device__ __forceinline__ void buf_st(u32x2 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, kAuxNT);
+}
+
+// Block prologue of both gathered kernels, three dependent latencies: the
+// stripe's descriptor index; the descriptor's first NDW dwords, one dword
+// per thread, into LDS; the stripe's source and output pointers (wave 0
+// and wave 1, selected by the descriptor) into LDS.
+template <int NDW, int KMAX, int R>
+__device__ __forceinline__ bool gather_prologue(const GatherParams &p, uint32_t s, uint32_t k, uint32_t *dsc,
+                                                uint64_t *ptr, int sel_dw, int dsel_dw) {
+    const uint32_t di = gather_desc(p, s);
+    if (di == kSkipStripe) return false;
+    const uint32_t *D = p.desc + size_t(di) * p.desc_dw;
+    constexpr int NI = (NDW + kThreads - 1) / kThreads;
+    uint32_t v[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int q = int(threadIdx.x) + i * kThreads;
+        v[i] = q < NDW ? D[q] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int q = int(threadIdx.x) + i * kThreads;
+        if (q < NDW) dsc[q] = v[i];
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < int(k)) {
+        const uint32_t sel = (dsc[sel_dw + t / 4] >> (8 * (t % 4))) & 0xffu;
+        ptr[t] = p.stab[uint64_t(s) * p.sstride + sel];
+    } else if (t >= 64 && t < 64 + R) {
+        const uint32_t sel = (dsc[dsel_dw] >> (8 * (t - 64))) & 0xffu;
+        ptr[KMAX + t - 64] = sel == kNoRow ? 0 : p.dtab[uint64_t(s) * p.dstride + sel];
+    }
+    __syncthreads();
+    return true;
+}
+
+template <int K, int R>
+__global__ __launch_bounds__(kThreads) void gf8_gather_kernel(const GatherParams p) {
+    constexpr int NDW = kGf8DescHead + R * K * 8;
+    __shared__ uint32_t dsc[NDW];
+    __shared__ uint64_t ptr[K + R];
+    const uint32_t local = blockIdx.x / p.tiles;
+    if (!gather_prologue<NDW, K, R>(p, p.s0 + local, K, dsc, ptr, 8, 16)) return;
+    const uint32_t u = (blockIdx.x - local * p.tiles) * kThreads + threadIdx.x;
+    if (u >= p.units) return;
+    const uint32_t off = u * 16;
+    uint32_t ones[4], zeros[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        ones[w] = uniform32(dsc[w]);
+        zeros[w] = uniform32(dsc[4 + w]);
+    }
+
+    u32x4 d[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) d[j] = buf_ld<u32x4>(chunk_rsrc(uniform64(ptr[j]), p.chunk), off, true);
+    __amdgpu_buffer_rsrc_t dr[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(uniform64(ptr[K + i]), p.chunk);
+    u32x4 acc[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, false) : u32x4{0, 0, 0, 0};
+    const uint32_t *tb = dsc + kGf8DescHead + opaque_zero();
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const u32x4 x = d[j];
+        const u32x4 s0 = x & 0x07070707u;
+        const u32x4 s1 = (x >> 3) & 0x07070707u;
+        const u32x4 s2 = (x >> 6) & 0x03030303u;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int b = i * K + j;
+            if ((zeros[b / 32] >> (b % 32)) & 1u) continue;
+            if ((ones[b / 32] >> (b % 32)) & 1u) {
+                acc[i] ^= x;
+                continue;
+            }
+            const u32x4 tt = *reinterpret_cast<const u32x4 *>(tb + b * 8);
+            const uint32_t v = tb[b * 8 + 4];
+            acc[i].x = xor4(acc[i].x, __builtin_amdgcn_perm(tt.y, tt.x, s0.x), __builtin_amdgcn_perm(tt.w, tt.z, s1.x),
+                            __builtin_amdgcn_perm(v, v, s2.x));
+            acc[i].y = xor4(acc[i].y, __builtin_amdgcn_perm(tt.y, tt.x, s0.y), __builtin_amdgcn_perm(tt.w, tt.z, s1.y),
+                            __builtin_amdgcn_perm(v, v, s2.y));
+            acc[i].z = xor4(acc[i].z, __builtin_amdgcn_perm(tt.y, tt.x, s0.z), __builtin_amdgcn_perm(tt.w, tt.z, s1.z),
+                            __builtin_amdgcn_perm(v, v, s2.z));
+            acc[i].w = xor4(acc[i].w, __builtin_amdgcn_perm(tt.y, tt.x, s0.w), __builtin_amdgcn_perm(tt.w, tt.z, s1.w),
+                            __builtin_amdgcn_perm(v, v, s2.w));
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
+}
+
+template <int W, int R>
+__global__ __launch_bounds__(kThreads) void bm_gather_kernel(const GatherParams p) {
+    constexpr int VW = bm_vw<W>();
+    constexpr int UB = 4 * VW;
+    constexpr int ROWS = R * W;
+    constexpr int MW = (ROWS + 3) / 4;  // mask dwords used per source (of W stored)
+    constexpr int NDW = kBmDescHead + kMaxSrc * W;
+    typedef typename VecT<VW>::type vec;
+    __shared__ uint32_t dsc[NDW];
+    __shared__ uint64_t ptr[kMaxSrc + R];
+    const uint32_t local = blockIdx.x / p.tiles;
+    const uint32_t k = p.k;
+    if (!gather_prologue<NDW, kMaxSrc, R>(p, p.s0 + local, k, dsc, ptr, 0, 8)) return;
+    const uint32_t u = (blockIdx.x - local * p.tiles) * kThreads + threadIdx.x;
+    if (u >= p.units) return;
+    const uint32_t off = u * UB;
+    const uint32_t pk = uint32_t(p.packet);
+    __amdgpu_buffer_rsrc_t dr[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(uniform64(ptr[kMaxSrc + i]), p.chunk);
+    vec acc[ROWS];
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int l = 0; l < W; ++l) acc[i * W + l] = p.accumulate ? buf_ld<vec>(dr[i], off + l * pk, false) : vec(0);
+    vec d[W], nx[W];
+    {
+        const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(uniform64(ptr[0]), p.chunk);
+#pragma unroll
+        for (int x = 0; x < W; ++x) d[x] = buf_ld<vec>(sr, off + x * pk, true);
+    }
+    const uint32_t *mt = dsc + kBmDescHead + opaque_zero();
+    for (uint32_t j = 0; j < k; ++j) {
+        if (j + 1 < k) {
+            const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(uniform64(ptr[j + 1]), p.chunk);
+#pragma unroll
+            for (int x = 0; x < W; ++x) nx[x] = buf_ld<vec>(sr, off + x * pk, true);
+        }
+        uint32_t mw[MW];
+#pragma unroll
+        for (int q = 0; q < MW; ++q) mw[q] = uniform32(mt[j * W + q]);
+#pragma unroll
+        for (int r = 0; r < ROWS; ++r) {
+            const uint32_t mb = (mw[r / 4] >> (8 * (r % 4))) & 0xffu;
+#pragma unroll
+            for (int x = 0; x < W; ++x) {
+                const uint32_t m = 0u - ((mb >> x) & 1u);
+                acc[r] = and_xor(d[x], m, acc[r]);
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < W; ++x) d[x] = nx[x];
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int l = 0; l < W; ++l) buf_st(acc[i * W + l], dr[i], off + l * pk);
+}
+
+hipError_t launch_gather_tail(const GatherLaunch &L, bool bitmatrix, uint64_t off, hipStream_t stream);
+
+inline GatherParams gather_params(const GatherLaunch &L, const Geometry &g) {
+    GatherParams p;
+    p.stab = L.stab;
+    p.dtab = L.dtab;
+    p.desc = static_cast<const uint32_t *>(L.desc);
+    p.desc_dw = L.desc_dw;
+    p.pat = L.pat;
+    p.packet = L.w ? L.len : 0;
+    p.chunk = uint32_t(L.w ? L.len * uint64_t(L.w) : L.len);
+    p.sstride = L.sstride;
+    p.dstride = L.dstride;
+    p.s0 = 0;
+    p.units = g.units;
+    p.tiles = g.tiles;
+    p.k = uint32_t(L.k);
+    p.accumulate = L.accumulate ? 1u : 0u;
+    return p;
+}
+
+template <int K, int R>
+hipError_t run_gf8_gather(const GatherLaunch &L, hipStream_t stream) {
+    const Geometry g = geometry(L.len / 16);
+    GatherParams p = gather_params(L, g);
+    if (g.units > 0) {
+        for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
+            const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
+            p.s0 = s0;
+            hipLaunchKernelGGL((gf8_gather_kernel<K, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+    }
+    if (L.len % 16) return launch_gather_tail(L, false, uint64_t(g.units) * 16, stream);
+    return hipSuccess;
+}
+
+template <int W, int R>
+hipError_t run_bm_gather(const GatherLaunch &L, hipStream_t stream) {
+    constexpr int UB = 4 * bm_vw<W>();
+    const Geometry g = geometry(L.len / UB);
+    GatherParams p = gather_params(L, g);
+    if (g.units > 0) {
+        for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
+            const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
+            p.s0 = s0;
+            hipLaunchKernelGGL((bm_gather_kernel<W, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+    }
+    if (L.len % UB) return launch_gather_tail(L, true, uint64_t(g.units) * UB, stream);
+    return hipSuccess;
+}
+
+#define MEC_GG8_ONE(K, R) template hipError_t run_gf8_gather<K, R>(const GatherLaunch &, hipStream_t);
+#define MEC_GG8_INSTANTIATE_LO(R)                                                                              \
+    MEC_GG8_ONE(1, R) MEC_GG8_ONE(2, R) MEC_GG8_ONE(3, R) MEC_GG8_ONE(4, R) MEC_GG8_ONE(5, R) MEC_GG8_ONE(6, R) \
+    MEC_GG8_ONE(7, R) MEC_GG8_ONE(8, R) MEC_GG8_ONE(9, R) MEC_GG8_ONE(10, R) MEC_GG8_ONE(11, R)                \
+    MEC_GG8_ONE(12, R) MEC_GG8_ONE(13, R) MEC_GG8_ONE(14, R) MEC_GG8_ONE(15, R) MEC_GG8_ONE(16, R)
+#define MEC_GG8_INSTANTIATE_HI(R)                                                                          \
+    MEC_GG8_ONE(17, R) MEC_GG8_ONE(18, R) MEC_GG8_ONE(19, R) MEC_GG8_ONE(20, R) MEC_GG8_ONE(21, R)        \
+    MEC_GG8_ONE(22, R) MEC_GG8_ONE(23, R) MEC_GG8_ONE(24, R) MEC_GG8_ONE(25, R) MEC_GG8_ONE(26, R)        \
+    MEC_GG8_ONE(27, R) MEC_GG8_ONE(28, R) MEC_GG8_ONE(29, R) MEC_GG8_ONE(30, R) MEC_GG8_ONE(31, R)        \
+    MEC_GG8_ONE(32, R)
+#define MEC_GBM_INSTANTIATE_W(W)                                                   \
+    template hipError_t run_bm_gather<W, 1>(const GatherLaunch &, hipStream_t); \
+    template hipError_t run_bm_gather<W, 2>(const GatherLaunch &, hipStream_t); \
+    template hipError_t run_bm_gather<W, 3>(const GatherLaunch &, hipStream_t); \
+    template hipError_t run_bm_gather<W, 4>(const GatherLaunch &, hipStream_t);
+
+}  // namespace detail
+}  // namespace mec

@@ -26,8 +26,6 @@ struct Gf8Params {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
-    const uint64_t *tab;  // gather mode: per stripe [K sources | dsts] chunk pointers
-    uint32_t tstride, tdst;
     uint32_t units, tiles, accumulate, pad;
     uint32_t ones[4], zeros[4];  // bit i*K+j: coefficient (i, j) is 1 / 0
     int64_t src_off[K];
@@ -48,9 +46,7 @@ __device__ __forceinline__ uint32_t gf8_mul(const Gf8Coef &c, uint32_t x) {
            __builtin_amdgcn_perm(c.v, c.v, (x >> 6) & 0x03030303u);
 }
 
-// G = gather: chunk addresses come from a per-stripe pointer table (scalar
-// loads, uniform per block) instead of base + stripe * stride + offset.
-template <int K, int R, bool G>
+template <int K, int R>
 __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) {
     __shared__ uint32_t tab[R * K * 8];
     for (int t = threadIdx.x; t < R * K; t += kThreads) {
@@ -66,37 +62,16 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
     const uint32_t u = (blockIdx.x - stripe * p.tiles) * kThreads + threadIdx.x;
     if (u >= p.units) return;
     const uint64_t off = uint64_t(u) * 16;
-    const uint8_t *sb = nullptr;
-    uint8_t *db = nullptr;
-    const uint64_t *row = nullptr;
-    if constexpr (G) {
-        row = p.tab + uint64_t(stripe) * p.tstride;
-    } else {
-        sb = p.src + int64_t(stripe) * p.sss + off;
-        db = p.dst + int64_t(stripe) * p.dss + off;
-    }
-    // kept as address expressions at the use sites: materialising pointer
-    // arrays costs the strided kernel 6 VGPRs and a wave per SIMD
-    auto sp = [&](int j) -> const uint8_t * {
-        if constexpr (G)
-            return reinterpret_cast<const uint8_t *>(row[j]) + off;
-        else
-            return sb + p.src_off[j];
-    };
-    auto dp = [&](int i) -> uint8_t * {
-        if constexpr (G)
-            return reinterpret_cast<uint8_t *>(row[p.tdst + i]) + off;
-        else
-            return db + p.dst_off[i];
-    };
+    const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
+    uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
 
     u32x4 d[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) d[j] = ld_nt<u32x4>(sp(j));
+    for (int j = 0; j < K; ++j) d[j] = ld_nt<u32x4>(sb + p.src_off[j]);
     u32x4 acc[R];
     if (p.accumulate) {
 #pragma unroll
-        for (int i = 0; i < R; ++i) acc[i] = *reinterpret_cast<const u32x4 *>(dp(i));
+        for (int i = 0; i < R; ++i) acc[i] = *reinterpret_cast<const u32x4 *>(db + p.dst_off[i]);
     } else {
 #pragma unroll
         for (int i = 0; i < R; ++i) acc[i] = u32x4{0, 0, 0, 0};
@@ -130,7 +105,7 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
         }
     }
 #pragma unroll
-    for (int i = 0; i < R; ++i) st_nt<u32x4>(dp(i), acc[i]);
+    for (int i = 0; i < R; ++i) st_nt<u32x4>(db + p.dst_off[i], acc[i]);
 }
 
 // The < 16-byte remainder of each region (chunk sizes that are not a
@@ -139,8 +114,6 @@ struct Gf8TailParams {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
-    const uint64_t *tab;
-    uint32_t tstride, tdst;
     uint64_t off;
     uint32_t n, k, rows, n_stripes, accumulate, pad;
     int64_t src_off[kMaxSrc];
@@ -155,8 +128,6 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     Gf8Params<K, R> p;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
-    p.tstride = L.tab_stride;
-    p.tdst = L.tab_dst;
     const Geometry g = geometry(L.len / 16);
     p.units = g.units;
     p.tiles = g.tiles;
@@ -175,17 +146,9 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     if (g.units > 0) {
         for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-            if (L.tab) {
-                p.src = nullptr;
-                p.dst = nullptr;
-                p.tab = L.tab + uint64_t(s0) * L.tab_stride;
-                hipLaunchKernelGGL((gf8_kernel<K, R, true>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-            } else {
-                p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-                p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-                p.tab = nullptr;
-                hipLaunchKernelGGL((gf8_kernel<K, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-            }
+            p.src = L.src + int64_t(s0) * L.src_stripe_stride;
+            p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+            hipLaunchKernelGGL((gf8_kernel<K, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

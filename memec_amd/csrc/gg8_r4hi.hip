@@ -1,0 +1,8 @@
+// gg8_r4hi.hip — gathered GF(2^8) kernel instantiations, 4 output row(s), K = 17..32.
+#include "gather_kernel.hpp"
+
+namespace mec {
+namespace detail {
+MEC_GG8_INSTANTIATE_HI(4)
+}  // namespace detail
+}  // namespace mec

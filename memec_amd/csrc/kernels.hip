@@ -25,6 +25,7 @@
 #include "kernels.hpp"
 #include "bm_kernel.hpp"
 #include "gf8_kernel.hpp"
+#include "gather_kernel.hpp"
 #include "stream_common.hpp"
 
 namespace mec {
@@ -33,6 +34,64 @@ template <int K, int R>
 hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream);
 template <int W, int R>
 hipError_t run_bm(const BmLaunch &L, hipStream_t stream);
+template <int K, int R>
+hipError_t run_gf8_gather(const GatherLaunch &L, hipStream_t stream);
+template <int W, int R>
+hipError_t run_bm_gather(const GatherLaunch &L, hipStream_t stream);
+
+// Gathered tails: the < unit remainder of each region, one thread per
+// stripe, any k / rows / w, reading the descriptor blob directly.
+__global__ __launch_bounds__(kThreads) void gather_tail_kernel(const GatherParams p, uint32_t n_stripes, uint32_t rows,
+                                                               uint32_t w, uint64_t off, uint32_t n, uint32_t bitmatrix) {
+    const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
+    if (s >= n_stripes) return;
+    const uint32_t di = gather_desc(p, s);
+    if (di == kSkipStripe) return;
+    const uint32_t *D = p.desc + size_t(di) * p.desc_dw;
+    const uint32_t sel_dw = bitmatrix ? 0 : 8, dsel_dw = bitmatrix ? 8 : 16;
+    const uint64_t *srow = p.stab + uint64_t(s) * p.sstride;
+    const uint64_t *drow = p.dtab + uint64_t(s) * p.dstride;
+    auto src = [&](uint32_t j, uint64_t extra) -> u32x4 {
+        const uint64_t a = srow[(D[sel_dw + j / 4] >> (8 * (j % 4))) & 0xffu];
+        return a ? load_partial(reinterpret_cast<const uint8_t *>(a) + off + extra, n) : u32x4{0, 0, 0, 0};
+    };
+    for (uint32_t i = 0; i < rows; ++i) {
+        const uint32_t sel = (D[dsel_dw] >> (8 * i)) & 0xffu;
+        if (sel == kNoRow || !drow[sel]) continue;
+        uint8_t *q0 = reinterpret_cast<uint8_t *>(drow[sel]) + off;
+        if (!bitmatrix) {
+            u32x4 acc = p.accumulate ? load_partial(q0, n) : u32x4{0, 0, 0, 0};
+            for (uint32_t j = 0; j < p.k; ++j) {
+                const u32x4 x = src(j, 0);
+                const uint32_t *t = D + kGf8DescHead + (i * p.k + j) * 8;
+                const Gf8Coef c{t[0], t[1], t[2], t[3], t[4]};
+                acc ^= u32x4{gf8_mul(c, x.x), gf8_mul(c, x.y), gf8_mul(c, x.z), gf8_mul(c, x.w)};
+            }
+            store_partial(q0, acc, n);
+        } else {
+            for (uint32_t l = 0; l < w; ++l) {
+                uint8_t *q = q0 + uint64_t(l) * p.packet;
+                u32x4 acc = p.accumulate ? load_partial(q, n) : u32x4{0, 0, 0, 0};
+                for (uint32_t j = 0; j < p.k; ++j) {
+                    const uint32_t r = i * w + l;
+                    const uint32_t mb = (D[kBmDescHead + j * w + r / 4] >> (8 * (r % 4))) & 0xffu;
+                    for (uint32_t x = 0; x < w; ++x)
+                        if ((mb >> x) & 1u) acc ^= src(j, uint64_t(x) * p.packet);
+                }
+                store_partial(q, acc, n);
+            }
+        }
+    }
+}
+
+hipError_t launch_gather_tail(const GatherLaunch &L, bool bitmatrix, uint64_t off, hipStream_t stream) {
+    Geometry g{};
+    GatherParams p = gather_params(L, g);
+    const uint32_t n = uint32_t(L.len - off);
+    hipLaunchKernelGGL(gather_tail_kernel, dim3((L.n_stripes + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, p,
+                       L.n_stripes, uint32_t(L.rows), uint32_t(L.w), off, n, bitmatrix ? 1u : 0u);
+    return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------
 // Tails: the < 16-byte (gf8) / < unit (bitmatrix) remainder of each region,
@@ -42,21 +101,16 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream);
 __global__ __launch_bounds__(kThreads) void gf8_tail_kernel(const Gf8TailParams p) {
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
     if (s >= p.n_stripes) return;
-    const uint64_t *row = p.tab ? p.tab + uint64_t(s) * p.tstride : nullptr;
-    auto srcp = [&](uint32_t j) -> const uint8_t * {
-        return row ? reinterpret_cast<const uint8_t *>(row[j]) + p.off : p.src + int64_t(s) * p.sss + p.off + p.src_off[j];
-    };
-    auto dstp = [&](uint32_t i) -> uint8_t * {
-        return row ? reinterpret_cast<uint8_t *>(row[p.tdst + i]) + p.off : p.dst + int64_t(s) * p.dss + p.off + p.dst_off[i];
-    };
+    const uint8_t *sb = p.src + int64_t(s) * p.sss + p.off;
+    uint8_t *db = p.dst + int64_t(s) * p.dss + p.off;
     for (uint32_t i = 0; i < p.rows; ++i) {
-        u32x4 acc = p.accumulate ? load_partial(dstp(i), p.n) : u32x4{0, 0, 0, 0};
+        u32x4 acc = p.accumulate ? load_partial(db + p.dst_off[i], p.n) : u32x4{0, 0, 0, 0};
         for (uint32_t j = 0; j < p.k; ++j) {
-            const u32x4 x = load_partial(srcp(j), p.n);
+            const u32x4 x = load_partial(sb + p.src_off[j], p.n);
             const Gf8Coef c = p.coef[i][j];
             acc ^= u32x4{gf8_mul(c, x.x), gf8_mul(c, x.y), gf8_mul(c, x.z), gf8_mul(c, x.w)};
         }
-        store_partial(dstp(i), acc, p.n);
+        store_partial(db + p.dst_off[i], acc, p.n);
     }
 }
 
@@ -66,9 +120,6 @@ hipError_t launch_gf8_tail(const Gf8Launch &L, uint64_t off, hipStream_t stream)
     p.dst = L.dst;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
-    p.tab = L.tab;
-    p.tstride = L.tab_stride;
-    p.tdst = L.tab_dst;
     p.off = off;
     p.n = uint32_t(L.len - off);
     p.k = uint32_t(L.k);
@@ -89,8 +140,6 @@ struct BmTailParams {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
-    const uint64_t *tab;
-    uint32_t tstride, tdst;
     uint64_t packet, off;
     uint32_t n, k, rows, w, n_stripes, accumulate;
     int64_t src_off[kMaxSrc];
@@ -101,21 +150,16 @@ struct BmTailParams {
 __global__ __launch_bounds__(kThreads) void bm_tail_kernel(const BmTailParams p) {
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
     if (s >= p.n_stripes) return;
-    const uint64_t *row = p.tab ? p.tab + uint64_t(s) * p.tstride : nullptr;
-    auto srcp = [&](uint32_t j) -> const uint8_t * {
-        return row ? reinterpret_cast<const uint8_t *>(row[j]) + p.off : p.src + int64_t(s) * p.sss + p.off + p.src_off[j];
-    };
-    auto dstp = [&](uint32_t i) -> uint8_t * {
-        return row ? reinterpret_cast<uint8_t *>(row[p.tdst + i]) + p.off : p.dst + int64_t(s) * p.dss + p.off + p.dst_off[i];
-    };
+    const uint8_t *sb = p.src + int64_t(s) * p.sss + p.off;
+    uint8_t *db = p.dst + int64_t(s) * p.dss + p.off;
     for (uint32_t i = 0; i < p.rows; ++i)
         for (uint32_t l = 0; l < p.w; ++l) {
-            uint8_t *q = dstp(i) + uint64_t(l) * p.packet;
+            uint8_t *q = db + p.dst_off[i] + uint64_t(l) * p.packet;
             u32x4 acc = p.accumulate ? load_partial(q, p.n) : u32x4{0, 0, 0, 0};
             for (uint32_t j = 0; j < p.k; ++j) {
                 const uint32_t mb = p.mask[j][i * p.w + l];
                 for (uint32_t x = 0; x < p.w; ++x)
-                    if ((mb >> x) & 1u) acc ^= load_partial(srcp(j) + uint64_t(x) * p.packet, p.n);
+                    if ((mb >> x) & 1u) acc ^= load_partial(sb + p.src_off[j] + uint64_t(x) * p.packet, p.n);
             }
             store_partial(q, acc, p.n);
         }
@@ -127,9 +171,6 @@ hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream) {
     p.dst = L.dst;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
-    p.tab = L.tab;
-    p.tstride = L.tab_stride;
-    p.tdst = L.tab_dst;
     p.packet = L.packet;
     p.off = off;
     p.n = uint32_t(L.packet - off);
@@ -182,6 +223,20 @@ constexpr std::array<BmFn, sizeof...(I)> make_bm_table(std::index_sequence<I...>
     return {{&run_bm<int(I / kMaxRows) + 1, int(I % kMaxRows) + 1>...}};
 }
 const auto kBmTable = make_bm_table(std::make_index_sequence<8 * kMaxRows>{});
+
+using GatherFn = hipError_t (*)(const GatherLaunch &, hipStream_t);
+
+template <size_t... I>
+constexpr std::array<GatherFn, sizeof...(I)> make_gg8_table(std::index_sequence<I...>) {
+    return {{&run_gf8_gather<int(I / kMaxRows) + 1, int(I % kMaxRows) + 1>...}};
+}
+const auto kGg8Table = make_gg8_table(std::make_index_sequence<kMaxSrc * kMaxRows>{});
+
+template <size_t... I>
+constexpr std::array<GatherFn, sizeof...(I)> make_gbm_table(std::index_sequence<I...>) {
+    return {{&run_bm_gather<int(I / kMaxRows) + 1, int(I % kMaxRows) + 1>...}};
+}
+const auto kGbmTable = make_gbm_table(std::make_index_sequence<8 * kMaxRows>{});
 
 // ---------------------------------------------------------------------------
 // XOR and fill
@@ -240,6 +295,22 @@ hipError_t launch_bm(const BmLaunch &L, hipStream_t stream) {
         return hipErrorInvalidValue;
     if (L.packet == 0 || L.n_stripes == 0) return hipSuccess;
     return kBmTable[size_t(L.w - 1) * kMaxRows + size_t(L.rows - 1)](L, stream);
+}
+
+hipError_t launch_gf8_gather(const GatherLaunch &L, hipStream_t stream) {
+    if (L.k < 1 || L.k > kMaxSrc || L.rows < 1 || L.rows > kMaxRows || !L.stab || !L.dtab || !L.desc)
+        return hipErrorInvalidValue;
+    if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
+    if (L.len / 16 > uint64_t(UINT32_MAX)) return hipErrorInvalidValue;
+    return kGg8Table[size_t(L.k - 1) * kMaxRows + size_t(L.rows - 1)](L, stream);
+}
+
+hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream) {
+    if (L.k < 1 || L.k > kMaxSrc || L.rows < 1 || L.rows > kMaxRows || L.w < 1 || L.w > 8 || !L.stab || !L.dtab ||
+        !L.desc)
+        return hipErrorInvalidValue;
+    if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
+    return kGbmTable[size_t(L.w - 1) * kMaxRows + size_t(L.rows - 1)](L, stream);
 }
 
 hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, hipStream_t stream) {

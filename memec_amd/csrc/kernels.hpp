@@ -19,19 +19,11 @@ struct Gf8Coef {
 };
 Gf8Coef gf8_coef(uint8_t c);
 
-// Chunk addressing of a launch.  Strided: source j of stripe s is
-// src + s * src_stripe_stride + src_off[j] (dst likewise).  Gather (tab !=
-// nullptr, a device array): stripe s's chunk pointers are the row
-// tab[s * tab_stride ...]: sources at [0, k), outputs at [tab_dst, tab_dst +
-// rows); src / dst / strides / offsets are then unused.
-
 // out[r] (^)= sum_j coef[r][j] * src[j]  over GF(2^8), byte-wise.
 struct Gf8Launch {
     const uint8_t *src;
     uint8_t *dst;
     int64_t src_stripe_stride, dst_stripe_stride;
-    const uint64_t *tab;
-    uint32_t tab_stride, tab_dst;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[kMaxRows];
     int k, rows;
@@ -48,8 +40,6 @@ struct BmLaunch {
     const uint8_t *src;
     uint8_t *dst;
     int64_t src_stripe_stride, dst_stripe_stride;
-    const uint64_t *tab;
-    uint32_t tab_stride, tab_dst;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[kMaxRows];
     int k, rows, w;        // rows = output chunks (each w packets)
@@ -59,7 +49,43 @@ struct BmLaunch {
     uint8_t mask[kMaxSrc][kMaxBmRows];
 };
 
+// ---- gathered launches (pointer-array batches) -------------------------------
+// A stripe's chunks are found through device tables of chunk pointers (one
+// row per stripe, as server/ holds Chunk* arrays) and its linear map through
+// a descriptor in device memory, so stripes with different erasure patterns
+// (decode) or delta columns (update) share one launch.
+constexpr uint8_t kNoRow = 0xFF;
+constexpr uint16_t kSkipStripe = 0xFFFF;
+
+// Descriptor blobs (uint32 words), one per map, desc_dw words apart:
+//  gf8 (K sources, 4 rows): [0..3] ones bits, [4..7] zeros bits (bit i*K+j),
+//      [8..15] ssel bytes, [16] dsel bytes (kNoRow = no output), then at
+//      kGf8DescHead + (i*K + j)*8 the v_perm tables t0 t1 u0 u1 v of
+//      coefficient (i, j);  desc_dw = kGf8DescHead + 4*K*8.
+//  bitmatrix (K sources, width w, 4 rows): [0..7] ssel bytes, [8] dsel bytes,
+//      then at kBmDescHead + j*w + q the mask bytes 4q..4q+3 of source j
+//      (byte i*w + l: bit x set <=> packet x feeds output i packet l);
+//      desc_dw = kBmDescHead + kMaxSrc*w.
+constexpr int kGf8DescHead = 32;
+constexpr int kBmDescHead = 16;
+
+struct GatherLaunch {
+    const uint64_t *stab;  // source pointer rows: stripe s at stab + s * sstride (0 = all-zero chunk)
+    const uint64_t *dtab;  // output pointer rows (0 = output not wanted)
+    uint32_t sstride, dstride;
+    const void *desc;      // descriptor blobs of this row group (device)
+    uint32_t desc_dw;      // dwords per descriptor
+    const uint16_t *pat;   // per-stripe descriptor index, kSkipStripe = no work; nullptr = desc 0
+    uint32_t n_stripes;
+    int k, rows;           // sources per stripe, output rows of this launch
+    int w;                 // bitmatrix field width
+    uint64_t len;          // gf8: bytes per chunk; bitmatrix: packet bytes
+    bool accumulate;       // XOR into outputs
+};
+
 hipError_t launch_gf8(const Gf8Launch &L, hipStream_t stream);
+hipError_t launch_gf8_gather(const GatherLaunch &L, hipStream_t stream);
+hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream);
 hipError_t launch_bm(const BmLaunch &L, hipStream_t stream);
 hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, hipStream_t stream);
 hipError_t launch_fill(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_offset, hipStream_t stream);

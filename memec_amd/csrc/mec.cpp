@@ -48,7 +48,6 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
     if (nd == 0 || n_stripes == 0) return MEC_OK;
     if (ns == 0) {  // all-zero input: outputs are zero (or unchanged when accumulating)
         if (accumulate) return MEC_OK;
-        if (lay.tab) return fail(MEC_EINVAL, "internal: gathered launch without sources");
         for (uint32_t s = 0; s < n_stripes; ++s)
             for (size_t r = 0; r < nd; ++r)
                 HIP_TRY(hipMemsetAsync(lay.dst + int64_t(s) * lay.dss + lay.dst_off[r], 0, c->cs, stream));
@@ -62,18 +61,13 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
             L.dst = lay.dst;
             L.src_stripe_stride = lay.sss;
             L.dst_stripe_stride = lay.dss;
-            L.tab = lay.tab;
-            L.tab_stride = lay.tstride;
-            L.tab_dst = uint32_t(ns + r0);
             L.k = int(ns);
             L.rows = rows;
             L.len = c->cs;
             L.n_stripes = n_stripes;
             L.accumulate = accumulate;
-            if (!lay.tab) {
-                for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
-                for (int i = 0; i < rows; ++i) L.dst_off[i] = lay.dst_off[r0 + i];
-            }
+            for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
+            for (int i = 0; i < rows; ++i) L.dst_off[i] = lay.dst_off[r0 + i];
             for (int i = 0; i < rows; ++i)
                 for (size_t j = 0; j < ns; ++j) L.coef[i][j] = mec::gf8_coef(coef[(r0 + i) * ns + j]);
             HIP_TRY(mec::launch_gf8(L, stream));
@@ -84,19 +78,14 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
             L.dst = lay.dst;
             L.src_stripe_stride = lay.sss;
             L.dst_stripe_stride = lay.dss;
-            L.tab = lay.tab;
-            L.tab_stride = lay.tstride;
-            L.tab_dst = uint32_t(ns + r0);
             L.k = int(ns);
             L.rows = rows;
             L.w = int(c->w);
             L.packet = c->packet;
             L.n_stripes = n_stripes;
             L.accumulate = accumulate;
-            if (!lay.tab) {
-                for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
-                for (int i = 0; i < rows; ++i) L.dst_off[i] = lay.dst_off[r0 + i];
-            }
+            for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
+            for (int i = 0; i < rows; ++i) L.dst_off[i] = lay.dst_off[r0 + i];
             for (int i = 0; i < rows; ++i)
                 for (size_t j = 0; j < ns; ++j)
                     bit_block(f, coef[(r0 + i) * ns + j], c->w, &L.mask[j][i * c->w], 1);

@@ -130,21 +130,30 @@ def coalescer(fam, k, m, cs, threads, per_thread, max_batch):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--only", default="", help="comma list of test names to run")
     a = ap.parse_args()
     reps = 3 if a.quick else 10
     torch.cuda.set_device(0)
-    device_gather("rs", 10, 4, 1 << 20, 1024, 8, reps)
-    device_gather("rs", 10, 4, 1 << 20, 1024, 256, reps)
-    device_gather("rs", 8, 2, 4096, 65536, 8, reps)
-    device_gather("rs", 8, 2, 4096, 65536, 256, reps)
-    device_gather("cauchy", 12, 4, 65536, 4096, 8, reps)
-    for npat in (1, 4, 14, 64):
-        decode_mixed("rs", 10, 4, 65536, 4096, npat, reps)
-    decode_mixed("cauchy", 12, 4, 65536, 4096, 4, reps)
-    host_batch("rs", 8, 2, 4096, 16384, reps)
-    host_batch("rs", 10, 4, 1 << 20, 64, reps)
-    for mb in (0, 256):
-        coalescer("rs", 8, 2, 4096, 16, 200, mb)
+    tests = [
+        ("gather_rs1m_h8", lambda: device_gather("rs", 10, 4, 1 << 20, 1024, 8, reps)),
+        ("gather_rs1m_h256", lambda: device_gather("rs", 10, 4, 1 << 20, 1024, 256, reps)),
+        ("gather_rs4k_h8", lambda: device_gather("rs", 8, 2, 4096, 65536, 8, reps)),
+        ("gather_rs4k_h256", lambda: device_gather("rs", 8, 2, 4096, 65536, 256, reps)),
+        ("gather_crs64k_h8", lambda: device_gather("cauchy", 12, 4, 65536, 4096, 8, reps)),
+    ]
+    tests += [("decode_mixed_%d" % n, (lambda n=n: decode_mixed("rs", 10, 4, 65536, 4096, n, reps)))
+              for n in (1, 4, 14, 64)]
+    tests += [
+        ("decode_mixed_crs", lambda: decode_mixed("cauchy", 12, 4, 65536, 4096, 4, reps)),
+        ("host_rs4k", lambda: host_batch("rs", 8, 2, 4096, 16384, reps)),
+        ("host_rs1m", lambda: host_batch("rs", 10, 4, 1 << 20, 64, reps)),
+        ("coalesce_off", lambda: coalescer("rs", 8, 2, 4096, 16, 200, 0)),
+        ("coalesce_on", lambda: coalescer("rs", 8, 2, 4096, 16, 200, 256)),
+    ]
+    only = set(x for x in a.only.split(",") if x)
+    for name, fn in tests:
+        if not only or name in only:
+            fn()
 
 
 if __name__ == "__main__":
