@@ -269,14 +269,19 @@ struct SlotHold {
 int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, const void *dtab, uint32_t dstride,
                const uint16_t *pat, uint32_t n, hipStream_t st) {
     if (M.ssel.empty() || M.rows() == 0 || n == 0) return MEC_OK;
+    // a single map with no skipped stripe runs from kernel arguments;
+    // anything else through per-stripe descriptors
+    bool single = M.ssel.size() == 1;
+    if (single && pat)
+        for (uint32_t s = 0; s < n && single; ++s) single = pat[s] == 0;
     std::vector<uint32_t> descs;
     uint32_t desc_dw = 0;
-    const size_t groups = build_descs(c, M, descs, desc_dw);
+    const size_t groups = single ? 0 : build_descs(c, M, descs, desc_dw);
     const bool same = stab == dtab && sstride == dstride;
     std::vector<std::pair<const void *, size_t>> parts = {
         {stab, size_t(n) * sstride * 8},
         {same ? nullptr : dtab, same ? 0 : size_t(n) * dstride * 8},
-        {pat, pat ? size_t(n) * 2 : 0},
+        {single ? nullptr : pat, (pat && !single) ? size_t(n) * 2 : 0},
         {descs.data(), descs.size() * sizeof(uint32_t)}};
     SlotHold hold;
     hold.st = st;
@@ -284,16 +289,65 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
     int rc = table_upload(c, parts, hold.t, offs, st);
     if (rc != MEC_OK) return rc;
     uint8_t *dev = reinterpret_cast<uint8_t *>(hold.t->dev);
+    const uint64_t *dstab = reinterpret_cast<const uint64_t *>(dev + offs[0]);
+    const uint64_t *ddtab = reinterpret_cast<const uint64_t *>(dev + offs[same ? 0 : 1]);
+    const size_t rows = M.rows(), nm = M.ssel.size();
+    if (single) {
+        // one map for every stripe: the map goes in kernel arguments
+        // (gf8_kernel / bm_kernel gather mode), only the pointers are read
+        const std::vector<uint8_t> &ss = M.ssel[0], &ds = M.dsel[0];
+        const Mat &cf = M.coef[0];
+        for (size_t r0 = 0; r0 < ds.size(); r0 += kMaxRows) {
+            const int nr = int(std::min<size_t>(kMaxRows, ds.size() - r0));
+            if (c->byte_wise()) {
+                Gf8Launch L{};
+                L.stab = dstab;
+                L.dtab = ddtab;
+                L.sstride = sstride;
+                L.dstride = dstride;
+                L.k = int(M.K);
+                L.rows = nr;
+                L.len = c->cs;
+                L.n_stripes = n;
+                L.accumulate = M.accumulate;
+                for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
+                for (int i = 0; i < nr; ++i) {
+                    L.dst_off[i] = ds[r0 + i];
+                    for (uint32_t j = 0; j < M.K; ++j) L.coef[i][j] = gf8_coef(cf[(r0 + i) * M.K + j]);
+                }
+                HIP_TRY(launch_gf8(L, st));
+            } else {
+                const Field &f = Field::get(int(c->w));
+                BmLaunch L{};
+                L.stab = dstab;
+                L.dtab = ddtab;
+                L.sstride = sstride;
+                L.dstride = dstride;
+                L.k = int(M.K);
+                L.rows = nr;
+                L.w = int(c->w);
+                L.packet = c->packet;
+                L.n_stripes = n;
+                L.accumulate = M.accumulate;
+                for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
+                for (int i = 0; i < nr; ++i) {
+                    L.dst_off[i] = ds[r0 + i];
+                    for (uint32_t j = 0; j < M.K; ++j) bit_block(f, cf[(r0 + i) * M.K + j], c->w, &L.mask[j][i * c->w], 1);
+                }
+                HIP_TRY(launch_bm(L, st));
+            }
+        }
+        return MEC_OK;
+    }
     GatherLaunch L{};
-    L.stab = reinterpret_cast<const uint64_t *>(dev + offs[0]);
-    L.dtab = reinterpret_cast<const uint64_t *>(dev + offs[same ? 0 : 1]);
+    L.stab = dstab;
+    L.dtab = ddtab;
     L.sstride = sstride;
     L.dstride = dstride;
     L.pat = pat ? reinterpret_cast<const uint16_t *>(dev + offs[2]) : nullptr;
     L.n_stripes = n;
     L.k = int(M.K);
     L.accumulate = M.accumulate;
-    const size_t rows = M.rows(), nm = M.ssel.size();
     for (size_t g = 0; g < groups; ++g) {
         L.rows = int(std::min<size_t>(kMaxRows, rows - g * kMaxRows));
         L.desc = dev + offs[3] + g * nm * desc_dw * sizeof(uint32_t);
@@ -725,9 +779,17 @@ int mec_encode_update_batch(mec_ctx *c, const uint32_t *data_index, const uint8_
         M.accumulate = true;
         const std::vector<uint32_t> rows = bits_of(pm, c->m);
         const std::vector<uint8_t> ds(rows.begin(), rows.end());
-        for (uint32_t j = 0; j < c->k; ++j) M.add({0}, ds, encode_rows(c, rows, {j}));
+        std::vector<int> id_of(c->k, -1);
         std::vector<uint16_t> pat(n_stripes);
-        for (uint32_t s = 0; s < n_stripes; ++s) pat[s] = delta[s] ? uint16_t(data_index[s]) : kSkipStripe;
+        for (uint32_t s = 0; s < n_stripes; ++s) {
+            if (!delta[s]) {
+                pat[s] = kSkipStripe;
+                continue;
+            }
+            const uint32_t j = data_index[s];
+            if (id_of[j] < 0) id_of[j] = int(M.add({0}, ds, encode_rows(c, rows, {j})));
+            pat[s] = uint16_t(id_of[j]);
+        }
         return run_gather(c, M, delta, 1, parity, c->m, pat.data(), n_stripes, hipStream_t(stream));
     }
     GroupSet G;

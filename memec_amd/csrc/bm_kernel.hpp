@@ -45,6 +45,8 @@ struct BmParams {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
+    const uint64_t *stab, *dtab;  // gather mode, as Gf8Params
+    uint32_t sstride, dstride, chunk, s0;
     uint64_t packet;
     uint32_t units, tiles, k, accumulate;
     int64_t src_off[kMaxSrc];
@@ -57,7 +59,24 @@ constexpr int bm_vw() {
     return W <= 4 ? 4 : 2;
 }
 
-template <int W, int R>
+// acc[r] ^= AND of source packet x with the 0 / ~0 mask of bit x of the
+// (uniform) mask byte mb[r]: one v_bitop3_b32 per dword.
+template <int W, int ROWS, typename vec>
+__device__ __forceinline__ void bm_combine(const vec (&d)[W], vec (&acc)[ROWS], const uint8_t *mb) {
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+        const uint32_t b = mb[r];
+#pragma unroll
+        for (int x = 0; x < W; ++x) {
+            // 0 / ~0 from a kernel-argument bit (SALU); acc ^= d & m is one
+            // v_bitop3_b32 per dword on gfx950.
+            const uint32_t m = 0u - ((b >> x) & 1u);
+            acc[r] = and_xor(d[x], m, acc[r]);
+        }
+    }
+}
+
+template <int W, int R, bool G>
 __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
     constexpr int VW = bm_vw<W>();
     constexpr int ROWS = R * W;
@@ -65,47 +84,70 @@ __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
     const uint32_t stripe = blockIdx.x / p.tiles;
     const uint32_t u = (blockIdx.x - stripe * p.tiles) * kThreads + threadIdx.x;
     if (u >= p.units) return;
-    const uint64_t off = uint64_t(u) * (4 * VW);
-    const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
-    uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
-
     vec acc[ROWS];
-    if (p.accumulate) {
+    vec d[W], nx[W];
+    if constexpr (G) {
+        const uint32_t off = u * (4 * VW);
+        const uint32_t pk = uint32_t(p.packet);
+        const uint64_t s = p.s0 + stripe;
+        const uint64_t *srow = p.stab + s * p.sstride;
+        const uint64_t *drow = p.dtab + s * p.dstride;
+        __amdgpu_buffer_rsrc_t dr[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(drow[p.dst_off[i]], p.chunk);
 #pragma unroll
         for (int i = 0; i < R; ++i)
 #pragma unroll
-            for (int l = 0; l < W; ++l)
-                acc[i * W + l] = *reinterpret_cast<const vec *>(db + p.dst_off[i] + uint64_t(l) * p.packet);
-    } else {
+            for (int l = 0; l < W; ++l) acc[i * W + l] = p.accumulate ? buf_ld<vec>(dr[i], off + l * pk, false) : vec(0);
+        {
+            const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(srow[p.src_off[0]], p.chunk);
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) acc[r] = vec(0);
-    }
-    vec d[W], nx[W];
-#pragma unroll
-    for (int x = 0; x < W; ++x) d[x] = ld_nt<vec>(sb + p.src_off[0] + uint64_t(x) * p.packet);
-    for (uint32_t j = 0; j < p.k; ++j) {
-        if (j + 1 < p.k) {
-#pragma unroll
-            for (int x = 0; x < W; ++x) nx[x] = ld_nt<vec>(sb + p.src_off[j + 1] + uint64_t(x) * p.packet);
+            for (int x = 0; x < W; ++x) d[x] = buf_ld<vec>(sr, off + x * pk, true);
         }
+        for (uint32_t j = 0; j < p.k; ++j) {
+            if (j + 1 < p.k) {
+                const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(srow[p.src_off[j + 1]], p.chunk);
 #pragma unroll
-        for (int r = 0; r < ROWS; ++r) {
-            const uint32_t mb = p.mask[j][r];
-#pragma unroll
-            for (int x = 0; x < W; ++x) {
-                // 0 / ~0 from a kernel-argument bit (SALU); acc ^= d & m is one
-                // v_bitop3_b32 per dword on gfx950.
-                const uint32_t m = 0u - ((mb >> x) & 1u);
-                acc[r] = and_xor(d[x], m, acc[r]);
+                for (int x = 0; x < W; ++x) nx[x] = buf_ld<vec>(sr, off + x * pk, true);
             }
+            bm_combine<W, ROWS, vec>(d, acc, p.mask[j]);
+#pragma unroll
+            for (int x = 0; x < W; ++x) d[x] = nx[x];
         }
 #pragma unroll
-        for (int x = 0; x < W; ++x) d[x] = nx[x];
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int l = 0; l < W; ++l) buf_st(acc[i * W + l], dr[i], off + l * pk);
+    } else {
+        const uint64_t off = uint64_t(u) * (4 * VW);
+        const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
+        uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
+        if (p.accumulate) {
+#pragma unroll
+            for (int i = 0; i < R; ++i)
+#pragma unroll
+                for (int l = 0; l < W; ++l)
+                    acc[i * W + l] = *reinterpret_cast<const vec *>(db + p.dst_off[i] + uint64_t(l) * p.packet);
+        } else {
+#pragma unroll
+            for (int r = 0; r < ROWS; ++r) acc[r] = vec(0);
+        }
+#pragma unroll
+        for (int x = 0; x < W; ++x) d[x] = ld_nt<vec>(sb + p.src_off[0] + uint64_t(x) * p.packet);
+        for (uint32_t j = 0; j < p.k; ++j) {
+            if (j + 1 < p.k) {
+#pragma unroll
+                for (int x = 0; x < W; ++x) nx[x] = ld_nt<vec>(sb + p.src_off[j + 1] + uint64_t(x) * p.packet);
+            }
+            bm_combine<W, ROWS, vec>(d, acc, p.mask[j]);
+#pragma unroll
+            for (int x = 0; x < W; ++x) d[x] = nx[x];
+        }
+#pragma unroll
+        for (int i = 0; i < R; ++i)
+#pragma unroll
+            for (int l = 0; l < W; ++l) st_nt<vec>(db + p.dst_off[i] + uint64_t(l) * p.packet, acc[i * W + l]);
     }
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-#pragma unroll
-        for (int l = 0; l < W; ++l) st_nt<vec>(db + p.dst_off[i] + uint64_t(l) * p.packet, acc[i * W + l]);
 }
 
 hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream);
@@ -118,6 +160,12 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     p.dss = L.dst_stripe_stride;
     p.packet = L.packet;
     p.k = uint32_t(L.k);
+    p.stab = L.stab;
+    p.dtab = L.dtab;
+    p.sstride = L.sstride;
+    p.dstride = L.dstride;
+    p.chunk = uint32_t(L.packet * uint64_t(L.w));
+    p.s0 = 0;
     const Geometry g = geometry(L.packet / UB);
     p.units = g.units;
     p.tiles = g.tiles;
@@ -129,9 +177,14 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     if (g.units > 0) {
         for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-            p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-            p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-            hipLaunchKernelGGL((bm_kernel<W, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            if (L.stab) {
+                p.s0 = s0;
+                hipLaunchKernelGGL((bm_kernel<W, R, true>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            } else {
+                p.src = L.src + int64_t(s0) * L.src_stripe_stride;
+                p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+                hipLaunchKernelGGL((bm_kernel<W, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

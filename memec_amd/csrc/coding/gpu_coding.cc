@@ -9,6 +9,15 @@ static int adapter_device() {
     return e ? atoi(e) : 0;
 }
 
+// One instance is shared by every server worker thread (server.cc:107,
+// worker.cc:128-137), each issuing single-stripe calls; libmec coalesces
+// the calls that arrive while a batch is in flight into the next batch.
+// MEMEC_GPU_COALESCE = max requests per batch (0 = one launch per call).
+static unsigned adapter_coalesce() {
+    const char *e = getenv("MEMEC_GPU_COALESCE");
+    return e ? unsigned(atoi(e)) : 256u;
+}
+
 GpuMatrixCoding::GpuMatrixCoding(int family, const char *name, uint32_t k, uint32_t m, uint32_t chunkSize)
     : _name(name), _family(family), _k(k), _m(m), _chunkSize(chunkSize), _ctx(0) {
     // Parameter errors exit(-1) with a message, like rscoding.cc:26-29 and
@@ -18,6 +27,8 @@ GpuMatrixCoding::GpuMatrixCoding(int family, const char *name, uint32_t k, uint3
         fprintf(stderr, "%s: %s\n", _name, mec_last_error());
         exit(-1);
     }
+    if (mec_set_coalescing(_ctx, adapter_coalesce()) != MEC_OK)
+        fprintf(stderr, "%s: coalescing unavailable: %s\n", _name, mec_last_error());
 }
 
 GpuMatrixCoding::~GpuMatrixCoding() { mec_destroy(_ctx); }

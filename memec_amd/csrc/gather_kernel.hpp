@@ -45,30 +45,6 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 }
 __device__ __forceinline__ uint32_t uniform32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
-// One chunk as a buffer resource: a NULL chunk gets zero records, so its
-// loads return 0 and its stores are dropped by the range check — no
-// branches around the memory operations.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(uint64_t a, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(a), 0, a ? int(bytes) : 0, 0x00020000);
-}
-constexpr int kAuxNT = 2;  // non-temporal (streamed once)
-template <typename V>
-__device__ __forceinline__ V buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt);
-template <>
-__device__ __forceinline__ u32x4 buf_ld<u32x4>(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
-    return nt ? __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxNT) : __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-}
-template <>
-__device__ __forceinline__ u32x2 buf_ld<u32x2>(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
-    return nt ? __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxNT) : __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
-}
-__device__ __forceinline__ void buf_st(u32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxNT);
-}
-__device__ __forceinline__ void buf_st(u32x2 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, kAuxNT);
-}
-
 // Block prologue of both gathered kernels, three dependent latencies: the
 // stripe's descriptor index; the descriptor's first NDW dwords, one dword
 // per thread, into LDS; the stripe's source and output pointers (wave 0
@@ -130,33 +106,7 @@ __global__ __launch_bounds__(kThreads) void gf8_gather_kernel(const GatherParams
     u32x4 acc[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, false) : u32x4{0, 0, 0, 0};
-    const uint32_t *tb = dsc + kGf8DescHead + opaque_zero();
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const u32x4 x = d[j];
-        const u32x4 s0 = x & 0x07070707u;
-        const u32x4 s1 = (x >> 3) & 0x07070707u;
-        const u32x4 s2 = (x >> 6) & 0x03030303u;
-#pragma unroll
-        for (int i = 0; i < R; ++i) {
-            const int b = i * K + j;
-            if ((zeros[b / 32] >> (b % 32)) & 1u) continue;
-            if ((ones[b / 32] >> (b % 32)) & 1u) {
-                acc[i] ^= x;
-                continue;
-            }
-            const u32x4 tt = *reinterpret_cast<const u32x4 *>(tb + b * 8);
-            const uint32_t v = tb[b * 8 + 4];
-            acc[i].x = xor4(acc[i].x, __builtin_amdgcn_perm(tt.y, tt.x, s0.x), __builtin_amdgcn_perm(tt.w, tt.z, s1.x),
-                            __builtin_amdgcn_perm(v, v, s2.x));
-            acc[i].y = xor4(acc[i].y, __builtin_amdgcn_perm(tt.y, tt.x, s0.y), __builtin_amdgcn_perm(tt.w, tt.z, s1.y),
-                            __builtin_amdgcn_perm(v, v, s2.y));
-            acc[i].z = xor4(acc[i].z, __builtin_amdgcn_perm(tt.y, tt.x, s0.z), __builtin_amdgcn_perm(tt.w, tt.z, s1.z),
-                            __builtin_amdgcn_perm(v, v, s2.z));
-            acc[i].w = xor4(acc[i].w, __builtin_amdgcn_perm(tt.y, tt.x, s0.w), __builtin_amdgcn_perm(tt.w, tt.z, s1.w),
-                            __builtin_amdgcn_perm(v, v, s2.w));
-        }
-    }
+    MEC_GF8_COMBINE(K, R, d, acc, dsc + kGf8DescHead + opaque_zero(), ones, zeros);
 #pragma unroll
     for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
 }

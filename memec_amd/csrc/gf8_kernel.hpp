@@ -26,6 +26,10 @@ struct Gf8Params {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
+    // gather mode (G): source j of stripe s is chunk pointer
+    // stab[s * sstride + src_off[j]], output i is dtab[s * dstride + dst_off[i]]
+    const uint64_t *stab, *dtab;
+    uint32_t sstride, dstride, chunk, s0;
     uint32_t units, tiles, accumulate, pad;
     uint32_t ones[4], zeros[4];  // bit i*K+j: coefficient (i, j) is 1 / 0
     int64_t src_off[K];
@@ -46,7 +50,45 @@ __device__ __forceinline__ uint32_t gf8_mul(const Gf8Coef &c, uint32_t x) {
            __builtin_amdgcn_perm(c.v, c.v, (x >> 6) & 0x03030303u);
 }
 
-template <int K, int R>
+// acc[i] ^= sum_j coef(i, j) * d[j] for one 16-byte unit: TB = the LDS
+// v_perm tables (8 dwords per coefficient, b = i*K + j), ONES / ZEROS = the
+// unit / zero coefficient bits (uniform: SGPRs, so the skips are scalar
+// branches).  A macro, not a function: passing the arrays by reference
+// costs ~25 VGPRs (79 -> 101-106 at K=10, R=4) in hipcc 7.2.
+#define MEC_GF8_COMBINE(K, R, d, acc, TB, ONES, ZEROS)                                                           \
+    do {                                                                                                         \
+        const uint32_t *tb_ = (TB);                                                                              \
+        _Pragma("unroll") for (int j_ = 0; j_ < (K); ++j_) {                                                     \
+            const u32x4 x_ = d[j_];                                                                              \
+            const u32x4 s0_ = x_ & 0x07070707u;                                                                  \
+            const u32x4 s1_ = (x_ >> 3) & 0x07070707u;                                                           \
+            const u32x4 s2_ = (x_ >> 6) & 0x03030303u;                                                           \
+            _Pragma("unroll") for (int i_ = 0; i_ < (R); ++i_) {                                                 \
+                const int b_ = i_ * (K) + j_;                                                                    \
+                if (((ZEROS)[b_ / 32] >> (b_ % 32)) & 1u) continue;                                              \
+                if (((ONES)[b_ / 32] >> (b_ % 32)) & 1u) {                                                       \
+                    acc[i_] ^= x_;                                                                               \
+                    continue;                                                                                    \
+                }                                                                                                \
+                const u32x4 t_ = *reinterpret_cast<const u32x4 *>(tb_ + b_ * 8);                                 \
+                const uint32_t v_ = tb_[b_ * 8 + 4];                                                             \
+                acc[i_].x = xor4(acc[i_].x, __builtin_amdgcn_perm(t_.y, t_.x, s0_.x),                            \
+                                 __builtin_amdgcn_perm(t_.w, t_.z, s1_.x), __builtin_amdgcn_perm(v_, v_, s2_.x)); \
+                acc[i_].y = xor4(acc[i_].y, __builtin_amdgcn_perm(t_.y, t_.x, s0_.y),                            \
+                                 __builtin_amdgcn_perm(t_.w, t_.z, s1_.y), __builtin_amdgcn_perm(v_, v_, s2_.y)); \
+                acc[i_].z = xor4(acc[i_].z, __builtin_amdgcn_perm(t_.y, t_.x, s0_.z),                            \
+                                 __builtin_amdgcn_perm(t_.w, t_.z, s1_.z), __builtin_amdgcn_perm(v_, v_, s2_.z)); \
+                acc[i_].w = xor4(acc[i_].w, __builtin_amdgcn_perm(t_.y, t_.x, s0_.w),                            \
+                                 __builtin_amdgcn_perm(t_.w, t_.z, s1_.w), __builtin_amdgcn_perm(v_, v_, s2_.w)); \
+            }                                                                                                    \
+        }                                                                                                        \
+    } while (0)
+
+// G = gather: chunk addresses come from per-stripe pointer rows (the
+// caller's Chunk* arrays) instead of base + stripe * stride + offset; the
+// map stays in kernel arguments, so a block's only extra latency is one
+// batch of scalar loads of its pointers.
+template <int K, int R, bool G>
 __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) {
     __shared__ uint32_t tab[R * K * 8];
     for (int t = threadIdx.x; t < R * K; t += kThreads) {
@@ -61,51 +103,40 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
     const uint32_t stripe = blockIdx.x / p.tiles;
     const uint32_t u = (blockIdx.x - stripe * p.tiles) * kThreads + threadIdx.x;
     if (u >= p.units) return;
-    const uint64_t off = uint64_t(u) * 16;
-    const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
-    uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
-
     u32x4 d[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) d[j] = ld_nt<u32x4>(sb + p.src_off[j]);
     u32x4 acc[R];
-    if (p.accumulate) {
+    if constexpr (G) {
+        const uint32_t off = u * 16;
+        const uint64_t s = p.s0 + stripe;
+        const uint64_t *srow = p.stab + s * p.sstride;
+        const uint64_t *drow = p.dtab + s * p.dstride;
 #pragma unroll
-        for (int i = 0; i < R; ++i) acc[i] = *reinterpret_cast<const u32x4 *>(db + p.dst_off[i]);
+        for (int j = 0; j < K; ++j) d[j] = buf_ld<u32x4>(chunk_rsrc(srow[p.src_off[j]], p.chunk), off, true);
+        __amdgpu_buffer_rsrc_t dr[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(drow[p.dst_off[i]], p.chunk);
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, false) : u32x4{0, 0, 0, 0};
+        MEC_GF8_COMBINE(K, R, d, acc, tab + opaque_zero(), p.ones, p.zeros);
+#pragma unroll
+        for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
     } else {
+        const uint64_t off = uint64_t(u) * 16;
+        const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
+        uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
 #pragma unroll
-        for (int i = 0; i < R; ++i) acc[i] = u32x4{0, 0, 0, 0};
-    }
-    const uint32_t *tb = tab + opaque_zero();
+        for (int j = 0; j < K; ++j) d[j] = ld_nt<u32x4>(sb + p.src_off[j]);
+        if (p.accumulate) {
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
-        const u32x4 x = d[j];
-        const u32x4 s0 = x & 0x07070707u;
-        const u32x4 s1 = (x >> 3) & 0x07070707u;
-        const u32x4 s2 = (x >> 6) & 0x03030303u;
+            for (int i = 0; i < R; ++i) acc[i] = *reinterpret_cast<const u32x4 *>(db + p.dst_off[i]);
+        } else {
 #pragma unroll
-        for (int i = 0; i < R; ++i) {
-            constexpr int kBits = 32;
-            const int b = i * K + j;
-            if ((p.zeros[b / kBits] >> (b % kBits)) & 1u) continue;
-            if ((p.ones[b / kBits] >> (b % kBits)) & 1u) {
-                acc[i] ^= x;
-                continue;
-            }
-            const u32x4 t = *reinterpret_cast<const u32x4 *>(tb + b * 8);
-            const uint32_t v = tb[b * 8 + 4];
-            acc[i].x = xor4(acc[i].x, __builtin_amdgcn_perm(t.y, t.x, s0.x), __builtin_amdgcn_perm(t.w, t.z, s1.x),
-                            __builtin_amdgcn_perm(v, v, s2.x));
-            acc[i].y = xor4(acc[i].y, __builtin_amdgcn_perm(t.y, t.x, s0.y), __builtin_amdgcn_perm(t.w, t.z, s1.y),
-                            __builtin_amdgcn_perm(v, v, s2.y));
-            acc[i].z = xor4(acc[i].z, __builtin_amdgcn_perm(t.y, t.x, s0.z), __builtin_amdgcn_perm(t.w, t.z, s1.z),
-                            __builtin_amdgcn_perm(v, v, s2.z));
-            acc[i].w = xor4(acc[i].w, __builtin_amdgcn_perm(t.y, t.x, s0.w), __builtin_amdgcn_perm(t.w, t.z, s1.w),
-                            __builtin_amdgcn_perm(v, v, s2.w));
+            for (int i = 0; i < R; ++i) acc[i] = u32x4{0, 0, 0, 0};
         }
-    }
+        MEC_GF8_COMBINE(K, R, d, acc, tab + opaque_zero(), p.ones, p.zeros);
 #pragma unroll
-    for (int i = 0; i < R; ++i) st_nt<u32x4>(db + p.dst_off[i], acc[i]);
+        for (int i = 0; i < R; ++i) st_nt<u32x4>(db + p.dst_off[i], acc[i]);
+    }
 }
 
 // The < 16-byte remainder of each region (chunk sizes that are not a
@@ -114,6 +145,8 @@ struct Gf8TailParams {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
+    const uint64_t *stab, *dtab;
+    uint32_t sstride, dstride;
     uint64_t off;
     uint32_t n, k, rows, n_stripes, accumulate, pad;
     int64_t src_off[kMaxSrc];
@@ -128,6 +161,12 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     Gf8Params<K, R> p;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
+    p.stab = L.stab;
+    p.dtab = L.dtab;
+    p.sstride = L.sstride;
+    p.dstride = L.dstride;
+    p.chunk = uint32_t(L.len);
+    p.s0 = 0;
     const Geometry g = geometry(L.len / 16);
     p.units = g.units;
     p.tiles = g.tiles;
@@ -146,9 +185,14 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     if (g.units > 0) {
         for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-            p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-            p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-            hipLaunchKernelGGL((gf8_kernel<K, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            if (L.stab) {
+                p.s0 = s0;
+                hipLaunchKernelGGL((gf8_kernel<K, R, true>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            } else {
+                p.src = L.src + int64_t(s0) * L.src_stripe_stride;
+                p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+                hipLaunchKernelGGL((gf8_kernel<K, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }

@@ -101,16 +101,23 @@ hipError_t launch_gather_tail(const GatherLaunch &L, bool bitmatrix, uint64_t of
 __global__ __launch_bounds__(kThreads) void gf8_tail_kernel(const Gf8TailParams p) {
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
     if (s >= p.n_stripes) return;
-    const uint8_t *sb = p.src + int64_t(s) * p.sss + p.off;
-    uint8_t *db = p.dst + int64_t(s) * p.dss + p.off;
+    const uint8_t *sb = p.stab ? nullptr : p.src + int64_t(s) * p.sss + p.off;
+    uint8_t *db = p.stab ? nullptr : p.dst + int64_t(s) * p.dss + p.off;
     for (uint32_t i = 0; i < p.rows; ++i) {
-        u32x4 acc = p.accumulate ? load_partial(db + p.dst_off[i], p.n) : u32x4{0, 0, 0, 0};
+        uint8_t *q = db ? db + p.dst_off[i] : reinterpret_cast<uint8_t *>(p.dtab[uint64_t(s) * p.dstride + p.dst_off[i]]);
+        if (!q) continue;
+        if (!db) q += p.off;
+        u32x4 acc = p.accumulate ? load_partial(q, p.n) : u32x4{0, 0, 0, 0};
         for (uint32_t j = 0; j < p.k; ++j) {
-            const u32x4 x = load_partial(sb + p.src_off[j], p.n);
+            const uint8_t *a =
+                sb ? sb + p.src_off[j] : reinterpret_cast<const uint8_t *>(p.stab[uint64_t(s) * p.sstride + p.src_off[j]]);
+            if (!a) continue;
+            if (!sb) a += p.off;
+            const u32x4 x = load_partial(a, p.n);
             const Gf8Coef c = p.coef[i][j];
             acc ^= u32x4{gf8_mul(c, x.x), gf8_mul(c, x.y), gf8_mul(c, x.z), gf8_mul(c, x.w)};
         }
-        store_partial(db + p.dst_off[i], acc, p.n);
+        store_partial(q, acc, p.n);
     }
 }
 
@@ -120,6 +127,10 @@ hipError_t launch_gf8_tail(const Gf8Launch &L, uint64_t off, hipStream_t stream)
     p.dst = L.dst;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
+    p.stab = L.stab;
+    p.dtab = L.dtab;
+    p.sstride = L.sstride;
+    p.dstride = L.dstride;
     p.off = off;
     p.n = uint32_t(L.len - off);
     p.k = uint32_t(L.k);
@@ -140,6 +151,8 @@ struct BmTailParams {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
+    const uint64_t *stab, *dtab;
+    uint32_t sstride, dstride;
     uint64_t packet, off;
     uint32_t n, k, rows, w, n_stripes, accumulate;
     int64_t src_off[kMaxSrc];
@@ -150,16 +163,22 @@ struct BmTailParams {
 __global__ __launch_bounds__(kThreads) void bm_tail_kernel(const BmTailParams p) {
     const uint32_t s = blockIdx.x * kThreads + threadIdx.x;
     if (s >= p.n_stripes) return;
-    const uint8_t *sb = p.src + int64_t(s) * p.sss + p.off;
-    uint8_t *db = p.dst + int64_t(s) * p.dss + p.off;
+    const uint8_t *sb = p.stab ? nullptr : p.src + int64_t(s) * p.sss + p.off;
+    uint8_t *db = p.stab ? nullptr : p.dst + int64_t(s) * p.dss + p.off;
     for (uint32_t i = 0; i < p.rows; ++i)
         for (uint32_t l = 0; l < p.w; ++l) {
-            uint8_t *q = db + p.dst_off[i] + uint64_t(l) * p.packet;
+            uint8_t *q0 = db ? db + p.dst_off[i] : reinterpret_cast<uint8_t *>(p.dtab[uint64_t(s) * p.dstride + p.dst_off[i]]);
+            if (!q0) continue;
+            uint8_t *q = q0 + (db ? 0 : p.off) + uint64_t(l) * p.packet;
             u32x4 acc = p.accumulate ? load_partial(q, p.n) : u32x4{0, 0, 0, 0};
             for (uint32_t j = 0; j < p.k; ++j) {
+                const uint8_t *a = sb ? sb + p.src_off[j]
+                                      : reinterpret_cast<const uint8_t *>(p.stab[uint64_t(s) * p.sstride + p.src_off[j]]);
+                if (!a) continue;
+                if (!sb) a += p.off;
                 const uint32_t mb = p.mask[j][i * p.w + l];
                 for (uint32_t x = 0; x < p.w; ++x)
-                    if ((mb >> x) & 1u) acc ^= load_partial(sb + p.src_off[j] + uint64_t(x) * p.packet, p.n);
+                    if ((mb >> x) & 1u) acc ^= load_partial(a + uint64_t(x) * p.packet, p.n);
             }
             store_partial(q, acc, p.n);
         }
@@ -171,6 +190,10 @@ hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream) {
     p.dst = L.dst;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
+    p.stab = L.stab;
+    p.dtab = L.dtab;
+    p.sstride = L.sstride;
+    p.dstride = L.dstride;
     p.packet = L.packet;
     p.off = off;
     p.n = uint32_t(L.packet - off);

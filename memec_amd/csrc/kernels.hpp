@@ -19,11 +19,18 @@ struct Gf8Coef {
 };
 Gf8Coef gf8_coef(uint8_t c);
 
+// Chunk addressing: strided (src + s * src_stripe_stride + src_off[j]), or,
+// when stab != nullptr (device arrays of chunk pointers, one row per
+// stripe), gathered: source j = stab[s * sstride + src_off[j]], output r =
+// dtab[s * dstride + dst_off[r]] (0 = all-zero source / unwanted output).
+
 // out[r] (^)= sum_j coef[r][j] * src[j]  over GF(2^8), byte-wise.
 struct Gf8Launch {
     const uint8_t *src;
     uint8_t *dst;
     int64_t src_stripe_stride, dst_stripe_stride;
+    const uint64_t *stab, *dtab;
+    uint32_t sstride, dstride;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[kMaxRows];
     int k, rows;
@@ -40,6 +47,8 @@ struct BmLaunch {
     const uint8_t *src;
     uint8_t *dst;
     int64_t src_stripe_stride, dst_stripe_stride;
+    const uint64_t *stab, *dtab;
+    uint32_t sstride, dstride;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[kMaxRows];
     int k, rows, w;        // rows = output chunks (each w packets)

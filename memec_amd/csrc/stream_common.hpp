@@ -28,6 +28,30 @@ __device__ __forceinline__ void st_nt(uint8_t *p, V v) {
     __builtin_nontemporal_store(v, reinterpret_cast<V *>(p));
 }
 
+// One chunk as a buffer resource: a NULL chunk gets zero records, so its
+// loads return 0 and its stores are dropped by the range check — no
+// branches around the memory operations.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(uint64_t a, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(a), 0, a ? int(bytes) : 0, 0x00020000);
+}
+constexpr int kAuxNT = 2;  // non-temporal (streamed once)
+template <typename V>
+__device__ __forceinline__ V buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt);
+template <>
+__device__ __forceinline__ u32x4 buf_ld<u32x4>(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
+    return nt ? __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kAuxNT) : __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+template <>
+__device__ __forceinline__ u32x2 buf_ld<u32x2>(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
+    return nt ? __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxNT) : __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_st(u32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxNT);
+}
+__device__ __forceinline__ void buf_st(u32x2 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, kAuxNT);
+}
+
 // An SGPR zero the compiler cannot see through: offsetting the LDS table
 // base by it stops LLVM from hoisting every table read to the top of the
 // kernel (which cost 200+ VGPRs and 2x time in tools/microbench.hip).

@@ -312,3 +312,49 @@ def test_batch_errors():
     # decode: NULL chunk pointer in a stripe that needs decoding -> EINVAL for that stripe
     res = c.decode_batch([0] * 6, [0b111110])
     assert res == [_lib.MEC_EINVAL]
+
+
+@pytest.mark.parametrize("fam", FAMS)
+def test_decode_batch_single_pattern(fam):
+    """Every stripe has the same erasures: the map runs from kernel
+    arguments (gf8_kernel / bm_kernel gather mode) instead of descriptors."""
+    k, m, cs, n = 6, 3, 4104 if fam != "rs" else 4096, 24
+    if fam == "cauchy" and O.cauchy_getw(k, m, cs) < 0:
+        cs = 4096
+    rng = np.random.default_rng(21)
+    slots = rng.permutation(n * (k + m))
+    slab = Slab(n * (k + m), cs, 8, True, 777)
+    before = slab.snapshot()
+    for pat in ([0, 4, 7], [8], [1, 2]):
+        slab.t.copy_(torch.from_numpy(before).to(DEV))
+        ptrs = [slab.addr(i) for s in range(n) for i in slots[s * (k + m):(s + 1) * (k + m)]]
+        mask = sum(1 << i for i in range(k + m) if i not in pat)
+        c = Codec(fam, k, m, cs)
+        assert c.decode_batch(ptrs, [mask] * n) == [0] * n
+        after = slab.snapshot()
+        for s in range(n):
+            row = slots[s * (k + m):(s + 1) * (k + m)]
+            chunks = [chunk_of(before, slab, i).copy() for i in row]
+            assert O.decode(fam, k, m, chunks, pat, cs) == 0
+            for i in range(k + m):
+                assert np.array_equal(chunk_of(after, slab, row[i]), chunks[i]), (fam, pat, s, i)
+
+
+@pytest.mark.parametrize("fam", ["rs", "cauchy"])
+def test_update_batch_single_column(fam):
+    k, m, cs, n, j = 5, 3, 2048, 16, 3
+    data = [O.fill(k * cs, 170 + s).reshape(k, cs) for s in range(n)]
+    parity0 = np.stack([np.stack(O.encode(fam, k, m, list(d), cs)) for d in data])
+    deltas = np.stack([O.fill(cs, 1900 + s) for s in range(n)])
+    P = torch.from_numpy(parity0.copy()).to(DEV)
+    D = torch.from_numpy(deltas).to(DEV)
+    c = Codec(fam, k, m, cs)
+    c.encode_update_batch([j] * n, [D.data_ptr() + s * cs for s in range(n)],
+                          [P.data_ptr() + (s * m + i) * cs for s in range(n) for i in range(m)], parity_mask=0b101)
+    got = P.cpu().numpy()
+    for s in range(n):
+        d2 = data[s].copy()
+        d2[j] ^= deltas[s]
+        want = O.encode(fam, k, m, list(d2), cs)
+        for i in range(m):
+            assert np.array_equal(got[s, i], want[i] if i != 1 else parity0[s, i]), (fam, s, i)
