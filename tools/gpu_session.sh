@@ -6,6 +6,7 @@
 #   benchall  bench.py for every config (no cpu baseline)
 #   batch   tools/bench_batch.py (pointer batches, coalescer)
 #   pmc     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench
+#   sq      rocprofv3 --pmc SQ_* pass (VALU/SALU instruction mix, occupancy)
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
@@ -49,6 +50,12 @@ for step in "$@"; do
                     -d "$OUT/pmc_fetch_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 5 --warmup 1
                 run "pmc_write_$c" 400 rocprofv3 --pmc WRITE_SIZE --output-format csv \
                     -d "$OUT/pmc_write_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 5 --warmup 1
+            done ;;
+        sq)
+            for c in ${PROF_CONFIGS:-rs_enc}; do
+                run "pmc_sq_$c" 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU \
+                    SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
+                    --output-format csv -d "$OUT/pmc_sq_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 3 --warmup 1
             done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
