@@ -100,7 +100,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed warmup steps (default: enough steps for >= 0.3 s of work, at least 3, "
+                         "so short configs run at a settled clock)")
     ap.add_argument("--config", default="rs_enc", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -155,6 +157,12 @@ def main():
             codec.decode(stripe, present)
         alg_bytes = (k + len(erased)) * cs * stripes
 
+    if args.warmup is None:  # size the warmup from one probe step
+        t0 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        probe = max(time.perf_counter() - t0, 1e-5)
+        args.warmup = int(min(2000, max(3, 0.3 / probe)))
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     wall, kern_ms = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize,
                                 dist=dist if world > 1 else None, events=ev)  # one launch per step

@@ -48,7 +48,7 @@ struct BmParams {
     const uint64_t *stab, *dtab;  // gather mode, as Gf8Params
     uint32_t sstride, dstride, chunk, s0;
     uint64_t packet;
-    uint32_t units, tiles, k, accumulate;
+    uint32_t units, tiles, k, accumulate, win, pad;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[R];
     uint8_t mask[kMaxSrc][R * W];
@@ -81,8 +81,9 @@ __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
     constexpr int VW = bm_vw<W>();
     constexpr int ROWS = R * W;
     typedef typename VecT<VW>::type vec;
-    const uint32_t stripe = blockIdx.x / p.tiles;
-    const uint32_t u = (blockIdx.x - stripe * p.tiles) * kThreads + threadIdx.x;
+    const uint32_t bid = block_order(p.win);
+    const uint32_t stripe = bid / p.tiles;
+    const uint32_t u = (bid - stripe * p.tiles) * kThreads + threadIdx.x;
     if (u >= p.units) return;
     vec acc[ROWS];
     vec d[W], nx[W];
@@ -170,6 +171,8 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     p.units = g.units;
     p.tiles = g.tiles;
     p.accumulate = L.accumulate ? 1u : 0u;
+    p.win = 1;
+    p.pad = 0;
     for (int j = 0; j < kMaxSrc; ++j) p.src_off[j] = j < L.k ? L.src_off[j] : 0;
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int j = 0; j < kMaxSrc; ++j)
@@ -183,6 +186,7 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
             } else {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+                p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
                 hipLaunchKernelGGL((bm_kernel<W, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
             }
             hipError_t e = hipGetLastError();

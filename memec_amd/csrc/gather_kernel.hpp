@@ -90,12 +90,6 @@ __global__ __launch_bounds__(kThreads) void gf8_gather_kernel(const GatherParams
     const uint32_t u = (blockIdx.x - local * p.tiles) * kThreads + threadIdx.x;
     if (u >= p.units) return;
     const uint32_t off = u * 16;
-    uint32_t ones[4], zeros[4];
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        ones[w] = uniform32(dsc[w]);
-        zeros[w] = uniform32(dsc[4 + w]);
-    }
 
     u32x4 d[K];
 #pragma unroll
@@ -106,7 +100,7 @@ __global__ __launch_bounds__(kThreads) void gf8_gather_kernel(const GatherParams
     u32x4 acc[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, false) : u32x4{0, 0, 0, 0};
-    MEC_GF8_COMBINE(K, R, d, acc, dsc + kGf8DescHead + opaque_zero(), ones, zeros);
+    gf8_apply<K, R, kGf8Dense>(d, acc, dsc + kGf8DescHead + opaque_zero());
 #pragma unroll
     for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
 }

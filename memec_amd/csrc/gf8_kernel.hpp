@@ -30,8 +30,7 @@ struct Gf8Params {
     // stab[s * sstride + src_off[j]], output i is dtab[s * dstride + dst_off[i]]
     const uint64_t *stab, *dtab;
     uint32_t sstride, dstride, chunk, s0;
-    uint32_t units, tiles, accumulate, pad;
-    uint32_t ones[4], zeros[4];  // bit i*K+j: coefficient (i, j) is 1 / 0
+    uint32_t units, tiles, accumulate, win;
     int64_t src_off[K];
     int64_t dst_off[R];
     Gf8Coef coef[R][K];
@@ -50,45 +49,94 @@ __device__ __forceinline__ uint32_t gf8_mul(const Gf8Coef &c, uint32_t x) {
            __builtin_amdgcn_perm(c.v, c.v, (x >> 6) & 0x03030303u);
 }
 
-// acc[i] ^= sum_j coef(i, j) * d[j] for one 16-byte unit: TB = the LDS
-// v_perm tables (8 dwords per coefficient, b = i*K + j), ONES / ZEROS = the
-// unit / zero coefficient bits (uniform: SGPRs, so the skips are scalar
-// branches).  A macro, not a function: passing the arrays by reference
-// costs ~25 VGPRs (79 -> 101-106 at K=10, R=4) in hipcc 7.2.
-#define MEC_GF8_COMBINE(K, R, d, acc, TB, ONES, ZEROS)                                                           \
-    do {                                                                                                         \
-        const uint32_t *tb_ = (TB);                                                                              \
-        _Pragma("unroll") for (int j_ = 0; j_ < (K); ++j_) {                                                     \
-            const u32x4 x_ = d[j_];                                                                              \
-            const u32x4 s0_ = x_ & 0x07070707u;                                                                  \
-            const u32x4 s1_ = (x_ >> 3) & 0x07070707u;                                                           \
-            const u32x4 s2_ = (x_ >> 6) & 0x03030303u;                                                           \
-            _Pragma("unroll") for (int i_ = 0; i_ < (R); ++i_) {                                                 \
-                const int b_ = i_ * (K) + j_;                                                                    \
-                if (((ZEROS)[b_ / 32] >> (b_ % 32)) & 1u) continue;                                              \
-                if (((ONES)[b_ / 32] >> (b_ % 32)) & 1u) {                                                       \
-                    acc[i_] ^= x_;                                                                               \
-                    continue;                                                                                    \
-                }                                                                                                \
-                const u32x4 t_ = *reinterpret_cast<const u32x4 *>(tb_ + b_ * 8);                                 \
-                const uint32_t v_ = tb_[b_ * 8 + 4];                                                             \
-                acc[i_].x = xor4(acc[i_].x, __builtin_amdgcn_perm(t_.y, t_.x, s0_.x),                            \
-                                 __builtin_amdgcn_perm(t_.w, t_.z, s1_.x), __builtin_amdgcn_perm(v_, v_, s2_.x)); \
-                acc[i_].y = xor4(acc[i_].y, __builtin_amdgcn_perm(t_.y, t_.x, s0_.y),                            \
-                                 __builtin_amdgcn_perm(t_.w, t_.z, s1_.y), __builtin_amdgcn_perm(v_, v_, s2_.y)); \
-                acc[i_].z = xor4(acc[i_].z, __builtin_amdgcn_perm(t_.y, t_.x, s0_.z),                            \
-                                 __builtin_amdgcn_perm(t_.w, t_.z, s1_.z), __builtin_amdgcn_perm(v_, v_, s2_.z)); \
-                acc[i_].w = xor4(acc[i_].w, __builtin_amdgcn_perm(t_.y, t_.x, s0_.w),                            \
-                                 __builtin_amdgcn_perm(t_.w, t_.z, s1_.w), __builtin_amdgcn_perm(v_, v_, s2_.w)); \
-            }                                                                                                    \
-        }                                                                                                        \
-    } while (0)
+// 3-input XOR of 16-byte vectors: one v_bitop3_b32 per dword.
+__device__ __forceinline__ u32x4 xor3(const u32x4 &a, const u32x4 &b, const u32x4 &c) {
+    return u32x4{uint32_t(__builtin_amdgcn_bitop3_b32(a.x, b.x, c.x, 0x96)),
+                 uint32_t(__builtin_amdgcn_bitop3_b32(a.y, b.y, c.y, 0x96)),
+                 uint32_t(__builtin_amdgcn_bitop3_b32(a.z, b.z, c.z, 0x96)),
+                 uint32_t(__builtin_amdgcn_bitop3_b32(a.w, b.w, c.w, 0x96))};
+}
+
+// Matrix structure a launch is specialised for (chosen on the host from the
+// coefficients, so the kernel has no data-dependent branches):
+//   kGf8Dense — every coefficient through its permute tables (a 0 / 1
+//               coefficient's tables give 0 / x, so any matrix is exact);
+//   kGf8Vand  — row 0 and column 0 all ones (Jerasure's Vandermonde
+//               distribution rows, reed_sol.c:269-297, and ISA-L's
+//               gf_gen_rs_matrix parity rows, ec_base.c:62-79): those
+//               entries are plain XORs, the rest through tables.
+constexpr int kGf8Dense = 0;
+constexpr int kGf8Vand = 1;
+
+// acc[i] ^= sum_j coef(i, j) * d[j] for one 16-byte unit.  TB = the LDS
+// permute tables (8 dwords per coefficient b = i*K + j: t0 t1 u0 u1 v).
+// Every product contributes 1 (unit) or 3 (v_perm) terms to its row; the
+// terms are folded into the row accumulator two at a time with 3-input
+// XORs, carrying an odd one over to the next source (the `has` flags are
+// compile-time constants once the loops are unrolled), so a table product
+// costs 3 v_perm + 1.5 v_bitop3 per dword and a unit one 0.5 v_bitop3.
+template <int K, int R, int S>
+__device__ __forceinline__ void gf8_apply(const u32x4 (&d)[K], u32x4 (&acc)[R], const uint32_t *tb) {
+    u32x4 pend[R];
+    bool has[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) has[i] = false;
+    auto put = [&](int i, const u32x4 &t) {
+        if (has[i]) {
+            acc[i] = xor3(acc[i], pend[i], t);
+            has[i] = false;
+        } else {
+            pend[i] = t;
+            has[i] = true;
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const u32x4 x = d[j];
+        if (S == kGf8Vand && j == 0) {
+#pragma unroll
+            for (int i = 0; i < R; ++i) put(i, x);
+            continue;
+        }
+        const u32x4 s0 = x & 0x07070707u;
+        const u32x4 s1 = (x >> 3) & 0x07070707u;
+        const u32x4 s2 = (x >> 6) & 0x03030303u;
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            if (S == kGf8Vand && i == 0) {
+                put(0, x);
+                continue;
+            }
+            const int b = i * K + j;
+            const u32x4 t = *reinterpret_cast<const u32x4 *>(tb + b * 8);
+            const uint32_t v = tb[b * 8 + 4];
+            put(i, u32x4{__builtin_amdgcn_perm(t.y, t.x, s0.x), __builtin_amdgcn_perm(t.y, t.x, s0.y),
+                         __builtin_amdgcn_perm(t.y, t.x, s0.z), __builtin_amdgcn_perm(t.y, t.x, s0.w)});
+            put(i, u32x4{__builtin_amdgcn_perm(t.w, t.z, s1.x), __builtin_amdgcn_perm(t.w, t.z, s1.y),
+                         __builtin_amdgcn_perm(t.w, t.z, s1.z), __builtin_amdgcn_perm(t.w, t.z, s1.w)});
+            put(i, u32x4{__builtin_amdgcn_perm(v, v, s2.x), __builtin_amdgcn_perm(v, v, s2.y),
+                         __builtin_amdgcn_perm(v, v, s2.z), __builtin_amdgcn_perm(v, v, s2.w)});
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+        if (has[i]) acc[i] ^= pend[i];
+}
+
+// Host side: the structure a coefficient block qualifies for.
+inline int gf8_structure(const Gf8Coef (*coef)[kMaxSrc], int k, int rows) {
+    const uint32_t one = 0x03020100u;  // t0 of coefficient 1 (identity on bits 0-2)
+    bool vand = true;
+    for (int j = 0; j < k && vand; ++j) vand = coef[0][j].t0 == one;
+    for (int i = 0; i < rows && vand; ++i) vand = coef[i][0].t0 == one;
+    return vand ? kGf8Vand : kGf8Dense;
+}
 
 // G = gather: chunk addresses come from per-stripe pointer rows (the
 // caller's Chunk* arrays) instead of base + stripe * stride + offset; the
 // map stays in kernel arguments, so a block's only extra latency is one
 // batch of scalar loads of its pointers.
-template <int K, int R, bool G>
+template <int K, int R, bool G, int S>
 __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) {
     __shared__ uint32_t tab[R * K * 8];
     for (int t = threadIdx.x; t < R * K; t += kThreads) {
@@ -100,8 +148,9 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
         tab[t * 8 + 4] = c.v;
     }
     __syncthreads();
-    const uint32_t stripe = blockIdx.x / p.tiles;
-    const uint32_t u = (blockIdx.x - stripe * p.tiles) * kThreads + threadIdx.x;
+    const uint32_t bid = block_order(p.win);
+    const uint32_t stripe = bid / p.tiles;
+    const uint32_t u = (bid - stripe * p.tiles) * kThreads + threadIdx.x;
     if (u >= p.units) return;
     u32x4 d[K];
     u32x4 acc[R];
@@ -117,7 +166,7 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
         for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(drow[p.dst_off[i]], p.chunk);
 #pragma unroll
         for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, false) : u32x4{0, 0, 0, 0};
-        MEC_GF8_COMBINE(K, R, d, acc, tab + opaque_zero(), p.ones, p.zeros);
+        gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
 #pragma unroll
         for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
     } else {
@@ -133,7 +182,7 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
 #pragma unroll
             for (int i = 0; i < R; ++i) acc[i] = u32x4{0, 0, 0, 0};
         }
-        MEC_GF8_COMBINE(K, R, d, acc, tab + opaque_zero(), p.ones, p.zeros);
+        gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
 #pragma unroll
         for (int i = 0; i < R; ++i) st_nt<u32x4>(db + p.dst_off[i], acc[i]);
     }
@@ -171,27 +220,29 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     p.units = g.units;
     p.tiles = g.tiles;
     p.accumulate = L.accumulate ? 1u : 0u;
-    p.pad = 0;
-    for (int w = 0; w < 4; ++w) p.ones[w] = p.zeros[w] = 0;
+    p.win = 1;
     for (int j = 0; j < K; ++j) p.src_off[j] = L.src_off[j];
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int i = 0; i < R; ++i)
-        for (int j = 0; j < K; ++j) {
-            p.coef[i][j] = L.coef[i][j];
-            const int b = i * K + j;
-            if (L.coef[i][j].t0 == 0x03020100u) p.ones[b / 32] |= 1u << (b % 32);
-            if (L.coef[i][j].t1 == 0) p.zeros[b / 32] |= 1u << (b % 32);
-        }
+        for (int j = 0; j < K; ++j) p.coef[i][j] = L.coef[i][j];
+    const bool vand = gf8_structure(L.coef, K, R) == kGf8Vand;
     if (g.units > 0) {
         for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
             if (L.stab) {
                 p.s0 = s0;
-                hipLaunchKernelGGL((gf8_kernel<K, R, true>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                if (vand)
+                    hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Vand>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                else
+                    hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Dense>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
             } else {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-                hipLaunchKernelGGL((gf8_kernel<K, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
+                if (vand)
+                    hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                else
+                    hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Dense>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
             }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;

@@ -19,6 +19,7 @@
 //  * xor_kernel — region XOR (Coding::bitwiseXOR, coding.cc:88-118).
 //  * fill_kernel — splitmix64 fill for synthetic stripes.
 #include <array>
+#include <cstdlib>
 #include <utility>
 
 #include "gf_math.hpp"
@@ -213,6 +214,17 @@ hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream) {
 }  // namespace detail
 
 using namespace detail;
+
+namespace detail {
+uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span) {
+    const char *e = std::getenv("MEC_WINDOWS");  // read per launch: experiments flip it
+    const int forced = e ? std::atoi(e) : 0;
+    if (forced > 0) return uint32_t(forced);
+    const int64_t a0 = int64_t(reinterpret_cast<uintptr_t>(src)), b0 = int64_t(reinterpret_cast<uintptr_t>(dst));
+    const int64_t a1 = a0 + std::max<int64_t>(src_span, 0), b1 = b0 + std::max<int64_t>(dst_span, 0);
+    return (b0 < a1 && a0 < b1) ? 2u : 1u;
+}
+}  // namespace detail
 
 Gf8Coef gf8_coef(uint8_t c) {
     const Field &f = Field::get(8);

@@ -61,6 +61,29 @@ __device__ __forceinline__ int opaque_zero() {
     return z;
 }
 
+// Block order.  Blocks are handed out in blockIdx order, so with the
+// identity map every resident block works inside one narrow address window
+// (a few consecutive stripes).  When the outputs are interleaved with the
+// inputs in that window (in-place decode of a [stripe][k+m][chunk] buffer,
+// parity written next to its data) the stream loses 6-8 % of HBM
+// throughput; splitting the grid into `win` windows far apart, taken
+// round-robin by consecutive block ids, recovers it (tools/layout_bench.hip,
+// tools/win_ab.py, profiles/r01/layout: RS(10,4) 1 MiB in-place decode
+// 73.4 % -> 79.5 % of 8 TB/s with 2 windows).  Separate input and output
+// buffers are already two windows: there a second split costs 4 % (RS(10,4)
+// encode 78.9 % -> 74.6 %), so they keep the identity order (win = 1).
+__device__ __forceinline__ uint32_t block_order(uint32_t win) {
+    const uint32_t b = blockIdx.x;
+    if (win <= 1) return b;
+    const uint32_t per = gridDim.x / win;
+    return b < per * win ? (b % win) * per + b / win : b;
+}
+
+// Host: windows for a strided launch — 2 when the output region lies inside
+// the input region's stripe span (one allocation, interleaved), else 1.
+// MEC_WINDOWS=<n> overrides (layout experiments).
+uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span);
+
 // ---------------------------------------------------------------------------
 // partial (tail) units: < 16 bytes at the end of a region
 // ---------------------------------------------------------------------------
