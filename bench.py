@@ -157,7 +157,9 @@ def main():
             codec.decode(stripe, present)
         alg_bytes = (k + len(erased)) * cs * stripes
 
-    if args.warmup is None:  # size the warmup from one probe step
+    if args.warmup is None:  # size the warmup from one probe step (after a first, cold one)
+        step()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
         step()
         torch.cuda.synchronize()
