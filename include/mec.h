@@ -73,7 +73,7 @@
 extern "C" {
 #endif
 
-#define MEC_ABI_VERSION 1
+#define MEC_ABI_VERSION 2
 #define MEC_MAX_CHUNKS 32 /* k + m <= 32: RS_N_MAX / CRS_N_MAX (rscoding.hh:5, cauchycoding.hh:5) */
 
 typedef enum {
@@ -104,6 +104,8 @@ typedef struct {
     uint64_t coalesced_batches;  /* batches run by the coalescer */
     uint64_t coalesced_requests; /* single-stripe requests they carried */
     uint64_t cached_plans;       /* decode plans cached (one per erasure pattern) */
+    uint64_t zero_copy_calls;    /* host calls coded in place over PCIe (registered memory) */
+    uint64_t staged_calls;       /* host calls staged through HBM */
 } mec_stats;
 
 typedef struct {
@@ -193,11 +195,21 @@ int mec_decode_host(mec_ctx *ctx, uint8_t *const *chunks, uint64_t present_mask)
 int mec_encode_update_host(mec_ctx *ctx, uint32_t data_index, const uint8_t *delta,
                            uint8_t *const *parity);
 
-/* Host-resident batch (dense [stripe][k][cs] data, [stripe][m][cs] parity),
- * pipelined H2D -> kernel -> D2H over internal streams; returns when the
- * parity is in host memory.  Pinned (mec_host_register) or pageable. */
+/* Host-resident batch (dense [stripe][k][cs] data, [stripe][m][cs] parity);
+ * returns when the parity is in host memory.  Registered memory (both
+ * buffers inside mec_host_register ranges) is coded zero-copy; otherwise
+ * pipelined H2D -> kernel -> D2H over internal streams. */
 int mec_encode_host_batch(mec_ctx *ctx, const uint8_t *data, uint8_t *parity,
                           uint32_t n_stripes, uint32_t parity_mask);
+
+/* Zero-copy host memory.  Pins [ptr, ptr + len) and maps it into the GPU's
+ * address space (hipHostRegister, mapped + portable).  Every host entry
+ * point (mec_*_host, mec_encode_host_batch, the pointer-array batches with
+ * MEC_MEM_HOST) whose chunks all lie in registered ranges runs its kernel
+ * directly on the host chunks over PCIe: no staging copy, one launch per
+ * call.  A server registers its ChunkPool slab once (chunk_pool.cc:22-47,
+ * the 8-byte chunk headers included); chunks outside registered ranges are
+ * staged through HBM as before.  mec_host_unregister takes the same ptr. */
 int mec_host_register(void *ptr, size_t len);
 int mec_host_unregister(void *ptr);
 
@@ -207,8 +219,9 @@ int mec_host_unregister(void *ptr);
  * c at array[s * chunks_per_row + c]), as the server holds Chunk* arrays.
  * mem_kind MEC_MEM_DEVICE: device pointers, work enqueued on `stream`
  * (the pointer arrays themselves are host arrays, consumed before return).
- * MEC_MEM_HOST: host pointers (pageable, or registered with
- * mec_host_register); staged through HBM, synchronous, `stream` ignored.
+ * MEC_MEM_HOST: host pointers; synchronous, `stream` ignored.  Zero-copy
+ * when every chunk lies in a mec_host_register range, otherwise staged
+ * through HBM.
  * Stripes are grouped by their linear map (same sources / outputs); each
  * group is one gather launch. */
 

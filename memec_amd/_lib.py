@@ -38,7 +38,8 @@ class MecInfo(ctypes.Structure):
 
 class MecStats(ctypes.Structure):
     _fields_ = [("coalesced_batches", ctypes.c_uint64), ("coalesced_requests", ctypes.c_uint64),
-                ("cached_plans", ctypes.c_uint64)]
+                ("cached_plans", ctypes.c_uint64), ("zero_copy_calls", ctypes.c_uint64),
+                ("staged_calls", ctypes.c_uint64)]
 
 
 _lib = None

@@ -191,7 +191,8 @@ class Codec:
         st = _lib.MecStats()
         check(lib().mec_get_stats(self._h, ctypes.byref(st)))
         return {"coalesced_batches": st.coalesced_batches, "coalesced_requests": st.coalesced_requests,
-                "cached_plans": st.cached_plans}
+                "cached_plans": st.cached_plans, "zero_copy_calls": st.zero_copy_calls,
+                "staged_calls": st.staged_calls}
 
 
 def fill_random(t, seed, word_offset=0, stream=None):

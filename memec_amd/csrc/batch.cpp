@@ -424,7 +424,54 @@ struct Item {
     bool direct;
 };
 
+// Zero-copy execution (hostmem.cpp): every chunk of every group lies in a
+// registered host range, so each group is one gathered launch over the
+// chunks' device addresses, on a lane stream; returns kNotZeroCopy (and
+// does nothing) otherwise.
+constexpr int kNotZeroCopy = 1;
+
+int run_zerocopy(mec_ctx *c, std::vector<Group> &gs) {
+    const size_t cs = c->cs;
+    std::vector<std::vector<uint64_t>> rows(gs.size());
+    for (size_t q = 0; q < gs.size(); ++q) {
+        rows[q] = gs[q].ptrs;
+        if (!zc_translate(rows[q].data(), rows[q].size(), cs)) return kNotZeroCopy;
+    }
+    int rc = MEC_OK;
+    LaneHold h{c, lane_acquire(c, rc)};
+    if (!h.l) return rc;
+    for (size_t q = 0; q < gs.size() && rc == MEC_OK; ++q) {
+        const Group &g = gs[q];
+        if (!g.n || !g.nd) continue;
+        const uint32_t row = g.ns + g.nd;
+        if (!g.ns) {  // every source is Coding::zeros: zero outputs (host pointers)
+            if (g.accumulate) continue;
+            for (uint32_t s = 0; s < g.n; ++s)
+                for (uint32_t r = 0; r < g.nd; ++r) std::memset(reinterpret_cast<void *>(g.ptrs[size_t(s) * row + g.ns + r]), 0, cs);
+            continue;
+        }
+        MapSet M;
+        M.K = g.ns;
+        M.accumulate = g.accumulate;
+        std::vector<uint8_t> ss(g.ns), ds(g.nd);
+        for (uint32_t j = 0; j < g.ns; ++j) ss[j] = uint8_t(j);
+        for (uint32_t i = 0; i < g.nd; ++i) ds[i] = uint8_t(g.ns + i);
+        M.add(ss, ds, g.coef);
+        rc = run_gather(c, M, rows[q].data(), row, rows[q].data(), row, nullptr, g.n, h.l->stream);
+    }
+    // no launch may outlive the call (the caller owns the chunks)
+    hipError_t e = hipStreamSynchronize(h.l->stream);
+    if (rc == MEC_OK && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+    if (rc == MEC_OK) c->zc_calls++;
+    return rc;
+}
+
 int run_host(mec_ctx *c, std::vector<Group> &gs) {
+    if (zc_any_registered()) {
+        const int zrc = run_zerocopy(c, gs);
+        if (zrc != kNotZeroCopy) return zrc;
+    }
+    c->staged_calls++;
     HostPipe &P = c->pipe;
     std::lock_guard<std::mutex> lk(P.mu);
     const size_t cs = c->cs;
@@ -813,6 +860,8 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
     std::lock_guard<std::mutex> lk(c->coal.mu);
     out->coalesced_batches = c->coal.batches;
     out->coalesced_requests = c->coal.requests;
+    out->zero_copy_calls = c->zc_calls.load();
+    out->staged_calls = c->staged_calls.load();
     {
         std::lock_guard<std::mutex> pk(c->plan_mu);
         out->cached_plans = c->plans.size();

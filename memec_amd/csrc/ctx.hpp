@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
@@ -119,6 +120,7 @@ struct mec_ctx {
     mec::core::TableSlot tabs[mec::core::kTableSlots];
     mec::core::HostPipe pipe;
     mec::core::Coalescer coal;
+    std::atomic<uint64_t> zc_calls{0}, staged_calls{0};  // host-call statistics
 
     bool byte_wise() const { return family != MEC_CAUCHY_GOOD; }
     mec::Scheme scheme() const {
@@ -187,6 +189,15 @@ struct LaneHold {
         if (l) lane_release(c, l);
     }
 };
+
+// hostmem.cpp: registered (GPU-mapped) host ranges.  zc_device_address:
+// device address of [p, p + len) if it lies in one registered range.
+// zc_translate: every non-zero entry of ptrs (chunks of len bytes) replaced
+// by its device address; false (ptrs partly rewritten) if any is not
+// registered.
+bool zc_device_address(const void *p, size_t len, uint64_t &dev);
+bool zc_any_registered();
+bool zc_translate(uint64_t *ptrs, size_t n, size_t len);
 
 // batch.cpp
 void batch_release(mec_ctx *c);  // frees table slots and the host pipeline

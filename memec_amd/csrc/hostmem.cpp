@@ -1,0 +1,95 @@
+// hostmem.cpp — host memory the GPU addresses directly (zero-copy).
+//
+// MemEC's chunks start and end in host memory (ChunkPool slabs fed from
+// sockets, chunk_pool.cc:22-95).  Host memory registered with
+// mec_host_register is mapped into the GPU's address space, so the coding
+// kernels read the k source chunks over PCIe and write the outputs straight
+// back — no staging copy through HBM and one launch per call.  Measured on
+// MI355X (tools/zerocopy_probe.hip, profiles/r01/zerocopy.log): the RS(10,4)
+// stream reads host memory at 54.7 GB/s of data (PCIe Gen5 x16 both ways)
+// against 40.4 GB/s for H2D + kernel + D2H, and a single RS(8,2) 4 KiB
+// stripe takes 13.5 us instead of 20.6 us.
+//
+// The registry maps registered host ranges to their device addresses; the
+// host entry points (mec_*_host, mec_*_batch with MEC_MEM_HOST,
+// mec_encode_host_batch) take the zero-copy path when every chunk of the
+// call lies in a registered range, and stage through HBM otherwise.
+#include <map>
+#include <shared_mutex>
+
+#include "ctx.hpp"
+
+namespace mec {
+namespace core {
+namespace {
+
+struct Range {
+    uintptr_t end;
+    uintptr_t dev;
+};
+
+std::shared_mutex reg_mu;
+std::map<uintptr_t, Range> reg;  // begin -> range
+
+}  // namespace
+
+bool zc_device_address(const void *p, size_t len, uint64_t &dev) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::shared_lock<std::shared_mutex> lk(reg_mu);
+    if (reg.empty()) return false;
+    auto it = reg.upper_bound(a);
+    if (it == reg.begin()) return false;
+    --it;
+    if (a < it->first || a + len > it->second.end) return false;
+    dev = uint64_t(it->second.dev + (a - it->first));
+    return true;
+}
+
+bool zc_any_registered() {
+    std::shared_lock<std::shared_mutex> lk(reg_mu);
+    return !reg.empty();
+}
+
+bool zc_translate(uint64_t *ptrs, size_t n, size_t len) {
+    if (!zc_any_registered()) return false;
+    for (size_t i = 0; i < n; ++i) {
+        if (!ptrs[i]) continue;  // NULL = zero source / unwanted output
+        uint64_t d;
+        if (!zc_device_address(reinterpret_cast<const void *>(uintptr_t(ptrs[i])), len, d)) return false;
+        ptrs[i] = d;
+    }
+    return true;
+}
+
+}  // namespace core
+}  // namespace mec
+
+using namespace mec::core;
+
+extern "C" {
+
+int mec_host_register(void *ptr, size_t len) {
+    if (!ptr || !len) return fail(MEC_EINVAL, "null or empty range");
+    HIP_TRY(hipHostRegister(ptr, len, hipHostRegisterMapped | hipHostRegisterPortable));
+    void *dev = nullptr;
+    hipError_t e = hipHostGetDevicePointer(&dev, ptr, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(ptr);
+        return hip_fail(e, "hipHostGetDevicePointer");
+    }
+    std::unique_lock<std::shared_mutex> lk(reg_mu);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    reg[a] = Range{a + len, reinterpret_cast<uintptr_t>(dev)};
+    return MEC_OK;
+}
+
+int mec_host_unregister(void *ptr) {
+    {
+        std::unique_lock<std::shared_mutex> lk(reg_mu);
+        reg.erase(reinterpret_cast<uintptr_t>(ptr));
+    }
+    HIP_TRY(hipHostUnregister(ptr));
+    return MEC_OK;
+}
+
+}  // extern "C"

@@ -166,6 +166,42 @@ void lane_release(mec_ctx *c, Lane *l) {
     c->lanes_free.push_back(l);
 }
 
+// Zero-copy single stripe (hostmem.cpp): when every source and output chunk
+// lies in a registered host range, one strided launch addresses the chunks
+// by their absolute device addresses (offsets from the first output) and
+// codes them in place over PCIe.  `taken` = false: not eligible, nothing
+// done.  No source (every data chunk is Coding::zeros) writes zero outputs.
+int zc_single(mec_ctx *c, const std::vector<const uint8_t *> &srcs, const std::vector<uint8_t *> &outs,
+              const Mat &coef, bool accumulate, bool &taken) {
+    taken = false;
+    if (outs.empty() || !zc_any_registered()) return MEC_OK;
+    const size_t cs = c->cs;
+    std::vector<uint64_t> a(srcs.size() + outs.size());
+    for (size_t t = 0; t < srcs.size(); ++t) a[t] = uint64_t(uintptr_t(srcs[t]));
+    for (size_t r = 0; r < outs.size(); ++r) a[srcs.size() + r] = uint64_t(uintptr_t(outs[r]));
+    if (!zc_translate(a.data(), a.size(), cs)) return MEC_OK;
+    taken = true;
+    if (srcs.empty()) {
+        if (!accumulate)
+            for (uint8_t *o : outs) std::memset(o, 0, cs);
+        return MEC_OK;
+    }
+    DeviceGuard dg(c->device);
+    int rc = MEC_OK;
+    LaneHold h{c, lane_acquire(c, rc)};
+    if (!h.l) return rc;
+    const uint64_t base = a[srcs.size()];
+    std::vector<int64_t> so(srcs.size()), dof(outs.size());
+    for (size_t t = 0; t < so.size(); ++t) so[t] = int64_t(a[t] - base);
+    for (size_t r = 0; r < dof.size(); ++r) dof[r] = int64_t(a[srcs.size() + r] - base);
+    uint8_t *b = reinterpret_cast<uint8_t *>(uintptr_t(base));
+    rc = apply(c, b, 0, so, b, 0, dof, coef, 1, accumulate, h.l->stream);
+    if (rc != MEC_OK) return rc;
+    HIP_TRY(hipStreamSynchronize(h.l->stream));
+    c->zc_calls++;
+    return MEC_OK;
+}
+
 
 }  // namespace core
 }  // namespace mec
@@ -359,18 +395,30 @@ int mec_fill_random(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_off
 int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *parity) {
     CHECK_CTX(c);
     if (!data || !parity) return fail(MEC_EINVAL, "null pointer array");
-    if (coalescing(c)) return submit_encode(c, data, parity);
-    DeviceGuard dg(c->device);
-    int rc = MEC_OK;
-    LaneHold h{c, lane_acquire(c, rc)};
-    if (!h.l) return rc;
-    const size_t cs = c->cs;
     std::vector<uint32_t> rows, cols;
     for (uint32_t i = 0; i < c->m; ++i)
         if (parity[i]) rows.push_back(i);
     if (rows.empty()) return MEC_OK;
     for (uint32_t j = 0; j < c->k; ++j)
         if (data[j]) cols.push_back(j);
+    {
+        std::vector<const uint8_t *> zs;
+        std::vector<uint8_t *> zo;
+        for (uint32_t j : cols) zs.push_back(data[j]);
+        for (uint32_t i : rows) zo.push_back(parity[i]);
+        bool taken;
+        int zrc = zc_single(c, zs, zo, encode_rows(c, rows, cols), false, taken);
+        if (taken) return zrc;
+    }
+    // staged calls are worth coalescing (one PCIe round trip per batch);
+    // zero-copy calls are not (they run concurrently on lane streams)
+    if (coalescing(c)) return submit_encode(c, data, parity);
+    c->staged_calls++;
+    DeviceGuard dg(c->device);
+    int rc = MEC_OK;
+    LaneHold h{c, lane_acquire(c, rc)};
+    if (!h.l) return rc;
+    const size_t cs = c->cs;
     std::vector<int64_t> so(cols.size()), dof(rows.size());
     for (size_t t = 0; t < cols.size(); ++t) {
         so[t] = int64_t(cols[t]) * int64_t(cs);
@@ -388,11 +436,23 @@ int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *pari
 int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
     CHECK_CTX(c);
     if (!chunks) return fail(MEC_EINVAL, "null pointer array");
-    if (coalescing(c)) return submit_decode(c, chunks, present_mask);
     std::shared_ptr<mec::LinearPlan> plan;
     int rc = get_plan(c, present_mask, plan);
     if (rc != MEC_OK) return rc;
     if (plan->dst.empty()) return MEC_OK;
+    for (uint32_t i = 0; i < c->k + c->m; ++i)
+        if (!chunks[i]) return fail(MEC_EINVAL, "chunk %u pointer is NULL", i);
+    {
+        std::vector<const uint8_t *> zs;
+        std::vector<uint8_t *> zo;
+        for (int t : plan->src) zs.push_back(chunks[t]);
+        for (int r : plan->dst) zo.push_back(chunks[r]);
+        bool taken;
+        int zrc = zc_single(c, zs, zo, plan->coef, false, taken);
+        if (taken) return zrc;
+    }
+    if (coalescing(c)) return submit_decode(c, chunks, present_mask);
+    c->staged_calls++;
     DeviceGuard dg(c->device);
     LaneHold h{c, lane_acquire(c, rc)};
     if (!h.l) return rc;
@@ -415,16 +475,24 @@ int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta
     CHECK_CTX(c);
     if (!delta || !parity) return fail(MEC_EINVAL, "null pointer");
     if (data_index >= c->k) return fail(MEC_EINVAL, "data_index %u >= k %u", data_index, c->k);
+    std::vector<uint32_t> rows, cols{data_index};
+    for (uint32_t i = 0; i < c->m; ++i)
+        if (parity[i]) rows.push_back(i);
+    if (rows.empty()) return MEC_OK;
+    {
+        std::vector<uint8_t *> zo;
+        for (uint32_t i : rows) zo.push_back(parity[i]);
+        bool taken;
+        int zrc = zc_single(c, {delta}, zo, encode_rows(c, rows, cols), true, taken);
+        if (taken) return zrc;
+    }
     if (coalescing(c)) return submit_update(c, data_index, delta, parity);
+    c->staged_calls++;
     DeviceGuard dg(c->device);
     int rc = MEC_OK;
     LaneHold h{c, lane_acquire(c, rc)};
     if (!h.l) return rc;
     const size_t cs = c->cs;
-    std::vector<uint32_t> rows, cols{data_index};
-    for (uint32_t i = 0; i < c->m; ++i)
-        if (parity[i]) rows.push_back(i);
-    if (rows.empty()) return MEC_OK;
     std::vector<int64_t> so{0}, dof(rows.size());
     HIP_TRY(hipMemcpyAsync(h.l->dev, delta, cs, hipMemcpyHostToDevice, h.l->stream));
     for (size_t r = 0; r < rows.size(); ++r) {
@@ -447,6 +515,26 @@ int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint
     std::lock_guard<std::mutex> bg(c->batch_mu);
     const size_t cs = c->cs, dbytes = size_t(c->k) * cs, pbytes = size_t(c->m) * cs;
     const size_t per = dbytes + pbytes;
+    for (int i = 0; i < 2; ++i)
+        if (!c->bstream[i]) HIP_TRY(hipStreamCreateWithFlags(&c->bstream[i], hipStreamNonBlocking));
+    uint64_t zd, zp;
+    if (n_stripes && zc_device_address(data, size_t(n_stripes) * dbytes, zd) &&
+        zc_device_address(parity, size_t(n_stripes) * pbytes, zp)) {
+        // zero-copy: one strided launch over the registered host buffers
+        std::vector<uint32_t> rows = mask_rows(c, parity_mask), cols(c->k);
+        for (uint32_t j = 0; j < c->k; ++j) cols[j] = j;
+        std::vector<int64_t> so(c->k), dof(rows.size());
+        for (uint32_t j = 0; j < c->k; ++j) so[j] = int64_t(j) * int64_t(cs);
+        for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(rows[r]) * int64_t(cs);
+        int rc = apply(c, reinterpret_cast<const uint8_t *>(uintptr_t(zd)), int64_t(dbytes), so,
+                       reinterpret_cast<uint8_t *>(uintptr_t(zp)), int64_t(pbytes), dof, encode_rows(c, rows, cols),
+                       n_stripes, false, c->bstream[0]);
+        if (rc != MEC_OK) return rc;
+        HIP_TRY(hipStreamSynchronize(c->bstream[0]));
+        c->zc_calls++;
+        return MEC_OK;
+    }
+    c->staged_calls++;
     const uint32_t sub = uint32_t(std::max<size_t>(1, std::min<size_t>(n_stripes, (size_t(256) << 20) / per)));
     const size_t need = size_t(sub) * per;
     if (c->bbytes < need) {
@@ -479,16 +567,6 @@ int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint
     }
     HIP_TRY(hipStreamSynchronize(c->bstream[0]));
     HIP_TRY(hipStreamSynchronize(c->bstream[1]));
-    return MEC_OK;
-}
-
-int mec_host_register(void *ptr, size_t len) {
-    HIP_TRY(hipHostRegister(ptr, len, hipHostRegisterDefault));
-    return MEC_OK;
-}
-
-int mec_host_unregister(void *ptr) {
-    HIP_TRY(hipHostUnregister(ptr));
     return MEC_OK;
 }
 

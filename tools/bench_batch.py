@@ -23,7 +23,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import Codec, fill_random, host_register, host_unregister  # noqa: E402
 
 
 def timed(fn, reps, warm=2):
@@ -85,29 +85,58 @@ def decode_mixed(fam, k, m, cs, n, n_patterns, reps):
     del stripe
 
 
-def host_batch(fam, k, m, cs, n, reps):
+def aligned(nbytes, align=4096):
+    raw = np.empty(nbytes + align, np.uint8)
+    off = (-raw.ctypes.data) % align
+    return raw[off:off + nbytes]
+
+
+def host_batch(fam, k, m, cs, n, reps, registered=False):
     c = Codec(fam, k, m, cs)
     slot = cs + 8
-    slab = np.random.default_rng(0).integers(0, 256, n * (k + m) * slot, dtype=np.uint8)
+    slab = aligned(n * (k + m) * slot)
+    slab[:] = np.random.default_rng(0).integers(0, 256, slab.size, dtype=np.uint8)
+    if registered:
+        host_register(slab)
     base = slab.ctypes.data
     rows = np.arange(n * (k + m), dtype=np.uint64).reshape(n, k + m) * np.uint64(slot) + np.uint64(base + 8)
     dptr = np.ascontiguousarray(rows[:, :k]).reshape(-1)
     pptr = np.ascontiguousarray(rows[:, k:]).reshape(-1)
     t = timed(lambda: c.encode_batch(dptr, pptr, mem="host"), reps, warm=1)
-    emit(test="host_encode_batch", family=fam, k=k, m=m, chunk=cs, stripes=n, memory="pageable",
-         ms=round(t * 1e3, 3), data_GiBps=round(gib(n * k * cs) / t, 2))
+    st = c.stats()
+    if registered:
+        host_unregister(slab)
+    emit(test="host_encode_batch", family=fam, k=k, m=m, chunk=cs, stripes=n,
+         memory="registered (zero-copy)" if registered else "pageable",
+         ms=round(t * 1e3, 3), data_GiBps=round(gib(n * k * cs) / t, 2),
+         zero_copy_calls=st["zero_copy_calls"], staged_calls=st["staged_calls"])
 
 
-def coalescer(fam, k, m, cs, threads, per_thread, max_batch):
+def coalescer(fam, k, m, cs, threads, per_thread, max_batch, registered=False):
+    """T threads issuing single-stripe mec_encode_host calls on their own
+    k + m chunks (slots of 8 + cs bytes in one slab, as ChunkPool)."""
+    import ctypes
+    from memec_amd._lib import lib
     c = Codec(fam, k, m, cs)
     if max_batch:
         c.set_coalescing(max_batch)
-    bufs = [[np.random.default_rng(t * 100 + j).integers(0, 256, cs, dtype=np.uint8) for j in range(k)]
-            for t in range(threads)]
+    slot = cs + 8
+    slab = aligned(threads * (k + m) * slot)
+    slab[:] = np.random.default_rng(1).integers(0, 256, slab.size, dtype=np.uint8)
+    if registered:
+        host_register(slab)
+    vp = ctypes.c_void_p
+    base = slab.ctypes.data
+    arrs = []
+    for t in range(threads):
+        a = [base + (t * (k + m) + i) * slot + 8 for i in range(k + m)]
+        arrs.append(((vp * k)(*[vp(x) for x in a[:k]]), (vp * m)(*[vp(x) for x in a[k:]])))
+    L = lib()
 
     def worker(t):
+        dp, pp = arrs[t]
         for _ in range(per_thread):
-            c.encode_host(bufs[t])
+            L.mec_encode_host(c._h, dp, pp)
 
     def run():
         th = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
@@ -121,10 +150,14 @@ def coalescer(fam, k, m, cs, threads, per_thread, max_batch):
     run()
     dt = time.perf_counter() - t0
     st = c.stats()
+    if registered:
+        host_unregister(slab)
     n = threads * per_thread
     emit(test="coalescer_encode_host", family=fam, k=k, m=m, chunk=cs, threads=threads, calls=n,
-         max_batch=max_batch, calls_per_s=round(n / dt, 1), data_GiBps=round(gib(n * k * cs) / dt, 3),
-         mean_batch=round(st["coalesced_requests"] / st["coalesced_batches"], 2) if st["coalesced_batches"] else 1)
+         max_batch=max_batch, memory="registered (zero-copy)" if registered else "pageable",
+         calls_per_s=round(n / dt, 1), data_GiBps=round(gib(n * k * cs) / dt, 3),
+         mean_batch=round(st["coalesced_requests"] / st["coalesced_batches"], 2) if st["coalesced_batches"] else 1,
+         zero_copy_calls=st["zero_copy_calls"], staged_calls=st["staged_calls"])
 
 
 def main():
@@ -147,8 +180,12 @@ def main():
         ("decode_mixed_crs", lambda: decode_mixed("cauchy", 12, 4, 65536, 4096, 4, reps)),
         ("host_rs4k", lambda: host_batch("rs", 8, 2, 4096, 16384, reps)),
         ("host_rs1m", lambda: host_batch("rs", 10, 4, 1 << 20, 64, reps)),
+        ("host_rs4k_reg", lambda: host_batch("rs", 8, 2, 4096, 16384, reps, True)),
+        ("host_rs1m_reg", lambda: host_batch("rs", 10, 4, 1 << 20, 64, reps, True)),
         ("coalesce_off", lambda: coalescer("rs", 8, 2, 4096, 16, 200, 0)),
         ("coalesce_on", lambda: coalescer("rs", 8, 2, 4096, 16, 200, 256)),
+        ("coalesce_off_reg", lambda: coalescer("rs", 8, 2, 4096, 16, 200, 0, True)),
+        ("coalesce_on_reg", lambda: coalescer("rs", 8, 2, 4096, 16, 200, 256, True)),
     ]
     only = set(x for x in a.only.split(",") if x)
     for name, fn in tests:

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "coding.hh"
+#include "mec.h"
 
 static Coding *coding;
 static uint32_t K, M, CS;
@@ -41,12 +42,28 @@ struct Worker {
     int id = 0;
 };
 
+static bool registered;  // MEMEC_GPU_REGISTER=1: chunks in a registered slab
+
 static void *run(void *arg) {
     Worker *w = (Worker *)arg;
     TempChunkPool pool;
     std::vector<Chunk *> c(K + M);
+    char *slab = 0;
+    const size_t slot = 8 + size_t(CS);
+    if (registered) {
+        // one ChunkPool-like slab per worker (slot = 8-byte header + data,
+        // chunk_pool.cc:22-47), mapped for zero-copy coding
+        slab = (char *)aligned_alloc(4096, ((K + M) * slot + 4095) / 4096 * 4096);
+        memset(slab, 0, (K + M) * slot);
+        if (mec_host_register(slab, (K + M) * slot) != MEC_OK) {
+            fprintf(stderr, "mec_host_register: %s\n", mec_last_error());
+            exit(1);
+        }
+        for (uint32_t i = 0; i < K + M; i++) c[i] = (Chunk *)(slab + i * slot);
+    } else {
+        for (auto &x : c) x = pool.alloc();
+    }
     for (auto &x : c) {
-        x = pool.alloc();
         char *d = ChunkUtil::getData(x);
         for (uint32_t b = 0; b < CS; b++) d[b] = char((b * 131 + w->id * 7) >> 3);
     }
@@ -78,7 +95,12 @@ static void *run(void *arg) {
         }
         it++;
     }
-    for (auto &x : c) pool.free(x);
+    if (registered) {
+        mec_host_unregister(slab);
+        free(slab);
+    } else {
+        for (auto &x : c) pool.free(x);
+    }
     return 0;
 }
 
@@ -100,6 +122,7 @@ int main(int argc, char **argv) {
     params.setM(M);
     params.setN(K + M);
     ChunkUtil::init(CS, K);
+    registered = getenv("MEMEC_GPU_REGISTER") && atoi(getenv("MEMEC_GPU_REGISTER"));
     coding = Coding::instantiate(scheme, params, CS);
     std::vector<Worker> ws(W);
     const double t0 = now();
@@ -121,8 +144,8 @@ int main(int argc, char **argv) {
     const double dt = now() - t0;
     const char *co = getenv("MEMEC_GPU_COALESCE");
     printf("{\"bench\": \"coding_adapter\", \"scheme\": \"%s\", \"k\": %u, \"m\": %u, \"chunk\": %u, \"workers\": %d, "
-           "\"mode\": \"%s\", \"coalesce\": %s, \"calls_per_s\": %.1f, \"data_GiBps\": %.4f}\n",
-           argv[1], K, M, CS, W, argv[7], co ? co : "256", calls / dt, bytes / dt / 1073741824.0);
+           "\"mode\": \"%s\", \"coalesce\": %s, \"registered\": %d, \"calls_per_s\": %.1f, \"data_GiBps\": %.4f}\n",
+           argv[1], K, M, CS, W, argv[7], co ? co : "256", registered ? 1 : 0, calls / dt, bytes / dt / 1073741824.0);
     Coding::destroy(coding);
     return 0;
 }

@@ -10,7 +10,9 @@ for cfg in "rs 8 2 4096" "rs 10 4 65536" "cauchy 12 4 65536"; do
   for mode in seal delta decode; do
     for w in 1 16; do
       for co in 0 256; do
-        MEMEC_GPU_COALESCE=$co timeout -k 10 120 tools/coding_bench $cfg $w $SECS $mode
+        for reg in ${REGISTER:-0 1}; do
+          MEMEC_GPU_REGISTER=$reg MEMEC_GPU_COALESCE=$co timeout -k 10 120 tools/coding_bench $cfg $w $SECS $mode
+        done
       done
     done
   done
