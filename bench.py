@@ -85,9 +85,12 @@ def cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads):
             "single_thread_value": round(single, 4), "matches_gpu": verified}
 
 
-def load_traffic(cfg_name):
+def load_traffic(cfg_name, stripes):
+    """PMC-measured HBM bytes per launch (profiles/pmc_<cfg>.json, written by
+    tools/pmc_summary.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
+    bench at the config's default stripe count); None for other sizes."""
     path = os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg_name)
-    if not os.path.exists(path):
+    if not os.path.exists(path) or stripes != CONFIGS[cfg_name][4]:
         return None
     try:
         with open(path) as f:
@@ -118,10 +121,19 @@ def main():
     from memec_amd.shard import dist_env, shard_range, timed_steps
 
     world, rank, local = dist_env()
+    # MEC_BENCH_DIST_BACKEND=gloo rehearses the multi-rank harness on fewer
+    # GPUs than ranks (ranks share devices round-robin); the real run is
+    # one rank per GPU over RCCL ("nccl").
+    backend = os.environ.get("MEC_BENCH_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     fam, k, m, cs, stripes, op, erased = CONFIGS[args.config]
     if args.stripes:
@@ -222,7 +234,7 @@ def main():
                        "chunk_bytes": cs, "stripes_per_gpu": stripes, "global_stripes": global_stripes,
                        "op": op, "erased": erased, "parallelism": "stripe-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, stripes),
                          "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4)},
             "cpu_baseline": None,
         }
