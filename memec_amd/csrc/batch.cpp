@@ -366,11 +366,10 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
 }
 
 // ---------------------------------------------------------------------------
-// host-memory execution: pack -> H2D -> kernel -> D2H -> unpack, two
-// buffers in flight
+// host-memory execution over unregistered chunks: pack into pinned,
+// GPU-mapped staging -> kernel over PCIe -> unpack, two buffers in flight
 // ---------------------------------------------------------------------------
-constexpr size_t kPipeBytes = size_t(64) << 20;   // per staging buffer
-constexpr size_t kDirectChunk = size_t(256) << 10; // chunks this large are DMA'd in place
+constexpr size_t kPipeBytes = size_t(64) << 20;  // per staging buffer
 
 struct Copy {
     void *dst;
@@ -406,13 +405,12 @@ int pipe_ready(mec_ctx *c, size_t bytes) {
     if (P.bytes >= bytes) return MEC_OK;
     for (int b = 0; b < 2; ++b) {
         if (P.host[b]) (void)hipHostFree(P.host[b]);
-        if (P.dev[b]) (void)hipFree(P.dev[b]);
-        P.host[b] = P.dev[b] = nullptr;
+        P.host[b] = P.hdev[b] = nullptr;
     }
     P.bytes = 0;
     for (int b = 0; b < 2; ++b) {
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&P.host[b]), bytes, hipHostMallocDefault));
-        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&P.dev[b]), bytes));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&P.host[b]), bytes, hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&P.hdev[b]), P.host[b], 0));
     }
     P.bytes = bytes;
     return MEC_OK;
@@ -421,7 +419,6 @@ int pipe_ready(mec_ctx *c, size_t bytes) {
 struct Item {
     Group *g;
     uint32_t s0, n;
-    bool direct;
 };
 
 // Zero-copy execution (hostmem.cpp): every chunk of every group lies in a
@@ -488,7 +485,7 @@ int run_host(mec_ctx *c, std::vector<Group> &gs) {
         const size_t per = size_t(g.ns + g.nd) * cs;
         need = std::max(need, per);
         const uint32_t sub = uint32_t(std::max<size_t>(1, kPipeBytes / per));
-        for (uint32_t s0 = 0; s0 < g.n; s0 += sub) items.push_back({&g, s0, std::min(sub, g.n - s0), cs >= kDirectChunk});
+        for (uint32_t s0 = 0; s0 < g.n; s0 += sub) items.push_back({&g, s0, std::min(sub, g.n - s0)});
     }
     if (items.empty()) return MEC_OK;
     int rc = pipe_ready(c, std::max(need, kPipeBytes));
@@ -498,55 +495,30 @@ int run_host(mec_ctx *c, std::vector<Group> &gs) {
     // staging layout: sources [n][ns][cs], then outputs [n][nd][cs]
     auto enqueue = [&](const Item &it, int b) -> int {
         const Group &g = *it.g;
-        uint8_t *h = P.host[b], *d = P.dev[b];
-        const size_t srcb = size_t(it.n) * g.ns * cs, outb = size_t(it.n) * g.nd * cs;
-        hipStream_t st = P.stream[b];
-        if (it.direct) {
-            for (uint32_t s = 0; s < it.n; ++s) {
-                const uint64_t *r = row(it, s);
-                for (uint32_t j = 0; j < g.ns; ++j)
-                    HIP_TRY(hipMemcpyAsync(d + (size_t(s) * g.ns + j) * cs, reinterpret_cast<const void *>(r[j]), cs,
-                                           hipMemcpyHostToDevice, st));
-                if (g.accumulate)
-                    for (uint32_t i = 0; i < g.nd; ++i)
-                        HIP_TRY(hipMemcpyAsync(d + srcb + (size_t(s) * g.nd + i) * cs,
-                                               reinterpret_cast<const void *>(r[g.ns + i]), cs, hipMemcpyHostToDevice, st));
-            }
-        } else {
-            std::vector<Copy> ops;
-            ops.reserve(size_t(it.n) * (g.ns + (g.accumulate ? g.nd : 0)));
-            for (uint32_t s = 0; s < it.n; ++s) {
-                const uint64_t *r = row(it, s);
-                for (uint32_t j = 0; j < g.ns; ++j)
-                    ops.push_back({h + (size_t(s) * g.ns + j) * cs, reinterpret_cast<const void *>(r[j])});
-                if (g.accumulate)
-                    for (uint32_t i = 0; i < g.nd; ++i)
-                        ops.push_back({h + srcb + (size_t(s) * g.nd + i) * cs, reinterpret_cast<const void *>(r[g.ns + i])});
-            }
-            copy_chunks(ops, cs);
-            HIP_TRY(hipMemcpyAsync(d, h, srcb + (g.accumulate ? outb : 0), hipMemcpyHostToDevice, st));
+        uint8_t *h = P.host[b], *d = P.hdev[b];
+        const size_t srcb = size_t(it.n) * g.ns * cs;
+        std::vector<Copy> ops;
+        ops.reserve(size_t(it.n) * (g.ns + (g.accumulate ? g.nd : 0)));
+        for (uint32_t s = 0; s < it.n; ++s) {
+            const uint64_t *r = row(it, s);
+            for (uint32_t j = 0; j < g.ns; ++j)
+                ops.push_back({h + (size_t(s) * g.ns + j) * cs, reinterpret_cast<const void *>(r[j])});
+            if (g.accumulate)
+                for (uint32_t i = 0; i < g.nd; ++i)
+                    ops.push_back({h + srcb + (size_t(s) * g.nd + i) * cs, reinterpret_cast<const void *>(r[g.ns + i])});
         }
+        copy_chunks(ops, cs);
         std::vector<int64_t> so(g.ns), dof(g.nd);
         for (uint32_t j = 0; j < g.ns; ++j) so[j] = int64_t(j) * int64_t(cs);
         for (uint32_t i = 0; i < g.nd; ++i) dof[i] = int64_t(i) * int64_t(cs);
-        int r = apply(c, d, int64_t(g.ns * cs), so, d + srcb, int64_t(g.nd * cs), dof, g.coef, it.n, g.accumulate, st);
+        int r = apply(c, d, int64_t(g.ns * cs), so, d + srcb, int64_t(g.nd * cs), dof, g.coef, it.n, g.accumulate,
+                      P.stream[b]);
         if (r != MEC_OK) return r;
-        if (it.direct) {
-            for (uint32_t s = 0; s < it.n; ++s) {
-                const uint64_t *rw = row(it, s);
-                for (uint32_t i = 0; i < g.nd; ++i)
-                    HIP_TRY(hipMemcpyAsync(reinterpret_cast<void *>(rw[g.ns + i]), d + srcb + (size_t(s) * g.nd + i) * cs,
-                                           cs, hipMemcpyDeviceToHost, st));
-            }
-        } else {
-            HIP_TRY(hipMemcpyAsync(h + srcb, d + srcb, outb, hipMemcpyDeviceToHost, st));
-        }
-        HIP_TRY(hipEventRecord(P.done[b], st));
+        HIP_TRY(hipEventRecord(P.done[b], P.stream[b]));
         return MEC_OK;
     };
     auto finish = [&](const Item &it, int b) -> int {
         HIP_TRY(hipEventSynchronize(P.done[b]));
-        if (it.direct) return MEC_OK;
         const Group &g = *it.g;
         const size_t srcb = size_t(it.n) * g.ns * cs;
         std::vector<Copy> ops;
@@ -693,7 +665,6 @@ void batch_release(mec_ctx *c) {
         }
         if (P.done[b]) (void)hipEventDestroy(P.done[b]);
         if (P.host[b]) (void)hipHostFree(P.host[b]);
-        if (P.dev[b]) (void)hipFree(P.dev[b]);
     }
 }
 

@@ -10,12 +10,15 @@ static int adapter_device() {
 }
 
 // One instance is shared by every server worker thread (server.cc:107,
-// worker.cc:128-137), each issuing single-stripe calls; libmec coalesces
-// the calls that arrive while a batch is in flight into the next batch.
-// MEMEC_GPU_COALESCE = max requests per batch (0 = one launch per call).
+// worker.cc:128-137), each issuing single-stripe calls.  Each call is one
+// launch on the calling thread's own stream, coding the chunks in place
+// (registered memory) or in mapped pinned staging, so concurrent calls
+// already overlap; batching them through the coalescer measured 2-4x
+// slower at 16 workers (profiles/r01/host/coding_bench_staged.jsonl), so
+// it is off unless MEMEC_GPU_COALESCE = max requests per batch is set.
 static unsigned adapter_coalesce() {
     const char *e = getenv("MEMEC_GPU_COALESCE");
-    return e ? unsigned(atoi(e)) : 256u;
+    return e ? unsigned(atoi(e)) : 0u;
 }
 
 GpuMatrixCoding::GpuMatrixCoding(int family, const char *name, uint32_t k, uint32_t m, uint32_t chunkSize)
@@ -27,7 +30,7 @@ GpuMatrixCoding::GpuMatrixCoding(int family, const char *name, uint32_t k, uint3
         fprintf(stderr, "%s: %s\n", _name, mec_last_error());
         exit(-1);
     }
-    if (mec_set_coalescing(_ctx, adapter_coalesce()) != MEC_OK)
+    if (adapter_coalesce() && mec_set_coalescing(_ctx, adapter_coalesce()) != MEC_OK)
         fprintf(stderr, "%s: coalescing unavailable: %s\n", _name, mec_last_error());
 }
 

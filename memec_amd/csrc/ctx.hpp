@@ -52,10 +52,14 @@ struct DeviceGuard {
 };
 
 // Staging resources for the single-stripe host entry points (one per
-// concurrent caller; server workers share one context, worker.cc:128-137).
+// concurrent caller; server workers share one context, worker.cc:128-137):
+// a stream and (k + m) chunk slots of pinned host memory mapped into the
+// GPU — unregistered chunks are copied into the slots and the kernel codes
+// them there over PCIe (no HBM round trip, one launch per call).
 struct Lane {
     hipStream_t stream = nullptr;
-    uint8_t *dev = nullptr;  // (k + m) chunk slots
+    uint8_t *host = nullptr;  // (k + m) chunk slots, pinned + mapped
+    uint8_t *hdev = nullptr;  // their device address
     size_t bytes = 0;
 };
 
@@ -72,15 +76,16 @@ struct TableSlot {
 };
 constexpr int kTableSlots = 4;
 
-// Double-buffered host pipeline of the host-memory pointer batches: chunks
-// are packed into pinned staging, moved with one DMA per sub-batch, coded
-// in HBM, and unpacked from pinned staging.
+// Double-buffered host pipeline of the host-memory pointer batches over
+// unregistered chunks: a sub-batch is packed into pinned, GPU-mapped
+// staging, coded there by the kernel over PCIe, and unpacked; packing the
+// next sub-batch overlaps the kernel on the current one.
 struct HostPipe {
     std::mutex mu;
     hipStream_t stream[2] = {nullptr, nullptr};
     hipEvent_t done[2] = {nullptr, nullptr};
-    uint8_t *host[2] = {nullptr, nullptr};
-    uint8_t *dev[2] = {nullptr, nullptr};
+    uint8_t *host[2] = {nullptr, nullptr};  // pinned + mapped
+    uint8_t *hdev[2] = {nullptr, nullptr};  // device addresses of host[]
     size_t bytes = 0;  // per buffer
 };
 

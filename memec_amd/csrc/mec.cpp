@@ -149,9 +149,11 @@ Lane *lane_acquire(mec_ctx *c, int &rc) {
     Lane *l = new Lane;
     l->bytes = size_t(c->k + c->m) * c->cs;
     hipError_t e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipMalloc(&l->dev, l->bytes);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&l->host), l->bytes, hipHostMallocMapped);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&l->hdev), l->host, 0);
     if (e != hipSuccess) {
         rc = hip_fail(e, "staging lane");
+        if (l->host) (void)hipHostFree(l->host);
         if (l->stream) (void)hipStreamDestroy(l->stream);
         delete l;
         return nullptr;
@@ -279,7 +281,7 @@ void mec_destroy(mec_ctx *c) {
         batch_release(c);
         for (Lane *l : c->lanes_all) {
             (void)hipStreamSynchronize(l->stream);
-            (void)hipFree(l->dev);
+            (void)hipHostFree(l->host);
             (void)hipStreamDestroy(l->stream);
             delete l;
         }
@@ -419,17 +421,20 @@ int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *pari
     LaneHold h{c, lane_acquire(c, rc)};
     if (!h.l) return rc;
     const size_t cs = c->cs;
+    if (cols.empty()) {  // every data chunk is Coding::zeros
+        for (uint32_t i : rows) std::memset(parity[i], 0, cs);
+        return MEC_OK;
+    }
     std::vector<int64_t> so(cols.size()), dof(rows.size());
     for (size_t t = 0; t < cols.size(); ++t) {
         so[t] = int64_t(cols[t]) * int64_t(cs);
-        HIP_TRY(hipMemcpyAsync(h.l->dev + so[t], data[cols[t]], cs, hipMemcpyHostToDevice, h.l->stream));
+        std::memcpy(h.l->host + so[t], data[cols[t]], cs);
     }
     for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(c->k + rows[r]) * int64_t(cs);
-    rc = apply(c, h.l->dev, 0, so, h.l->dev, 0, dof, encode_rows(c, rows, cols), 1, false, h.l->stream);
+    rc = apply(c, h.l->hdev, 0, so, h.l->hdev, 0, dof, encode_rows(c, rows, cols), 1, false, h.l->stream);
     if (rc != MEC_OK) return rc;
-    for (size_t r = 0; r < rows.size(); ++r)
-        HIP_TRY(hipMemcpyAsync(parity[rows[r]], h.l->dev + dof[r], cs, hipMemcpyDeviceToHost, h.l->stream));
     HIP_TRY(hipStreamSynchronize(h.l->stream));
+    for (size_t r = 0; r < rows.size(); ++r) std::memcpy(parity[rows[r]], h.l->host + dof[r], cs);
     return MEC_OK;
 }
 
@@ -460,14 +465,13 @@ int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
     std::vector<int64_t> so(plan->src.size()), dof(plan->dst.size());
     for (size_t t = 0; t < so.size(); ++t) {
         so[t] = int64_t(plan->src[t]) * int64_t(cs);
-        HIP_TRY(hipMemcpyAsync(h.l->dev + so[t], chunks[plan->src[t]], cs, hipMemcpyHostToDevice, h.l->stream));
+        std::memcpy(h.l->host + so[t], chunks[plan->src[t]], cs);
     }
     for (size_t r = 0; r < dof.size(); ++r) dof[r] = int64_t(plan->dst[r]) * int64_t(cs);
-    rc = apply(c, h.l->dev, 0, so, h.l->dev, 0, dof, plan->coef, 1, false, h.l->stream);
+    rc = apply(c, h.l->hdev, 0, so, h.l->hdev, 0, dof, plan->coef, 1, false, h.l->stream);
     if (rc != MEC_OK) return rc;
-    for (size_t r = 0; r < dof.size(); ++r)
-        HIP_TRY(hipMemcpyAsync(chunks[plan->dst[r]], h.l->dev + dof[r], cs, hipMemcpyDeviceToHost, h.l->stream));
     HIP_TRY(hipStreamSynchronize(h.l->stream));
+    for (size_t r = 0; r < dof.size(); ++r) std::memcpy(chunks[plan->dst[r]], h.l->host + dof[r], cs);
     return MEC_OK;
 }
 
@@ -494,16 +498,15 @@ int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta
     if (!h.l) return rc;
     const size_t cs = c->cs;
     std::vector<int64_t> so{0}, dof(rows.size());
-    HIP_TRY(hipMemcpyAsync(h.l->dev, delta, cs, hipMemcpyHostToDevice, h.l->stream));
+    std::memcpy(h.l->host, delta, cs);
     for (size_t r = 0; r < rows.size(); ++r) {
         dof[r] = int64_t(1 + r) * int64_t(cs);
-        HIP_TRY(hipMemcpyAsync(h.l->dev + dof[r], parity[rows[r]], cs, hipMemcpyHostToDevice, h.l->stream));
+        std::memcpy(h.l->host + dof[r], parity[rows[r]], cs);
     }
-    rc = apply(c, h.l->dev, 0, so, h.l->dev, 0, dof, encode_rows(c, rows, cols), 1, true, h.l->stream);
+    rc = apply(c, h.l->hdev, 0, so, h.l->hdev, 0, dof, encode_rows(c, rows, cols), 1, true, h.l->stream);
     if (rc != MEC_OK) return rc;
-    for (size_t r = 0; r < rows.size(); ++r)
-        HIP_TRY(hipMemcpyAsync(parity[rows[r]], h.l->dev + dof[r], cs, hipMemcpyDeviceToHost, h.l->stream));
     HIP_TRY(hipStreamSynchronize(h.l->stream));
+    for (size_t r = 0; r < rows.size(); ++r) std::memcpy(parity[rows[r]], h.l->host + dof[r], cs);
     return MEC_OK;
 }
 

@@ -866,3 +866,69 @@ int orc_encode_batch_mt(int family, int k, int m, uint32_t chunk_size,
     free(ops);
     return rc;
 }
+
+struct dec_job {
+    int family, k, m, w, rc;
+    uint32_t cs;
+    const int *matrix, *bm, *erased;
+    uint8_t *chunks;
+    uint32_t s0, s1;
+};
+
+static void *dec_worker(void *arg)
+{
+    struct dec_job *jb = (struct dec_job *)arg;
+    uint8_t *d[64], *p[64];
+    uint32_t s;
+    int i, n = jb->k + jb->m;
+    for (s = jb->s0; s < jb->s1; s++) {
+        for (i = 0; i < jb->k; i++) d[i] = jb->chunks + ((size_t)s * n + i) * jb->cs;
+        for (i = 0; i < jb->m; i++) p[i] = jb->chunks + ((size_t)s * n + jb->k + i) * jb->cs;
+        if (jb->family == 0) {
+            if (orc_rs_decode(jb->k, jb->m, jb->matrix, jb->erased, d, p, jb->cs)) jb->rc = -1;
+        } else {
+            if (orc_crs_decode(jb->k, jb->m, jb->w, jb->bm, jb->erased, d, p, jb->cs, jb->cs / jb->w)) jb->rc = -1;
+        }
+    }
+    return NULL;
+}
+
+/* Multi-threaded in-place decode of a dense [s][k+m][cs] batch, one erasure
+ * pattern (erased[i] != 0: chunk i lost) for every stripe; each stripe
+ * rebuilds its decoding matrix / schedule as the reference does per call
+ * (rscoding.cc:182 -> jerasure.c:223; cauchycoding.cc:173 -> jerasure.c:958).
+ * Threads take disjoint stripes (batch_performance.cc:143-154). */
+int orc_decode_batch_mt(int family, int k, int m, uint32_t chunk_size, uint8_t *chunks,
+                        uint32_t n_stripes, const int *erased, int threads)
+{
+    int matrix[32 * 32], *bm = NULL, w, t, rc = 0;
+    pthread_t tid[256];
+    struct dec_job jobs[256];
+
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_once(&g_mt8_once, mt8_build);
+    if (family == 0) {
+        w = orc_rs_getw((uint32_t)k, (uint32_t)m, chunk_size);
+        if (w != 8 || orc_rs_vandermonde_matrix(k, m, 8, matrix)) return -1;
+    } else {
+        w = orc_cauchy_getw((uint32_t)k, (uint32_t)m, chunk_size);
+        if (w < 1 || w > 8 || orc_cauchy_good_matrix(k, m, w, matrix)) return -1;
+        bm = malloc(sizeof(int) * (size_t)k * m * w * w);
+        orc_matrix_to_bitmatrix(k, m, w, matrix, bm);
+    }
+    for (t = 0; t < threads; t++) {
+        jobs[t].family = family; jobs[t].k = k; jobs[t].m = m; jobs[t].w = w; jobs[t].rc = 0;
+        jobs[t].cs = chunk_size; jobs[t].matrix = matrix; jobs[t].bm = bm; jobs[t].erased = erased;
+        jobs[t].chunks = chunks;
+        jobs[t].s0 = (uint32_t)((uint64_t)n_stripes * t / threads);
+        jobs[t].s1 = (uint32_t)((uint64_t)n_stripes * (t + 1) / threads);
+        if (pthread_create(&tid[t], NULL, dec_worker, &jobs[t])) { rc = -1; threads = t; break; }
+    }
+    for (t = 0; t < threads; t++) {
+        pthread_join(tid[t], NULL);
+        if (jobs[t].rc) rc = -1;
+    }
+    free(bm);
+    return rc;
+}

@@ -45,6 +45,8 @@ def lib():
                                              u8p, u8p, ctypes.POINTER(u8p)]
         L.orc_encode_batch_mt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
                                           u8p, u8p, ctypes.c_uint32, ctypes.c_int]
+        L.orc_decode_batch_mt.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint32,
+                                          u8p, ctypes.c_uint32, ip, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -159,6 +161,13 @@ def decode(family, k, m, chunks, erased, cs):
 def encode_batch_mt(family, k, m, cs, data, parity, n_stripes, threads):
     fam = 0 if family == "rs" else 1
     return lib().orc_encode_batch_mt(fam, k, m, cs, ptr(data), ptr(parity), n_stripes, threads)
+
+
+def decode_batch_mt(family, k, m, cs, chunks, n_stripes, erased, threads):
+    """In-place decode of dense [s][k+m][cs] stripes, one erasure pattern."""
+    fam = 0 if family == "rs" else 1
+    er = (ctypes.c_int * (k + m))(*[1 if i in erased else 0 for i in range(k + m)])
+    return lib().orc_decode_batch_mt(fam, k, m, cs, ptr(chunks), n_stripes, er, threads)
 
 
 _golden = None

@@ -118,7 +118,7 @@ def test_encode_batch_scattered(fam, mem, hdr):
 
 
 def test_encode_batch_parity_mask_and_big_chunks_host():
-    """RS(10,4)@1MiB on host memory (chunks >= 256 KiB are DMA'd in place)."""
+    """RS(10,4)@1MiB on host memory (staged through mapped pinned buffers)."""
     k, m, cs, n = 10, 4, 1 << 20, 3
     c = Codec("rs", k, m, cs)
     data = [O.fill(cs, 500 + i) for i in range(n * k)]

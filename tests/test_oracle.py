@@ -154,3 +154,24 @@ def test_roundtrip_every_pattern_small(fam):
                 assert O.decode(fam, k, m, chunks, list(pat), cs) == 0
                 for i in range(k + m):
                     assert np.array_equal(chunks[i], orig[i]), (fam, k, m, pat, i)
+
+
+@pytest.mark.parametrize("fam", ["rs", "cauchy"])
+def test_batch_mt_paths_match_single_stripe(fam):
+    """The CPU-baseline drivers (orc_encode_batch_mt / orc_decode_batch_mt,
+    threads on disjoint stripes) equal the single-stripe oracle."""
+    k, m, cs, n = 10, 4, 4096, 12
+    data = O.fill(n * k * cs, 31)
+    par = np.zeros(n * m * cs, np.uint8)
+    assert O.encode_batch_mt(fam, k, m, cs, data, par, n, 3) == 0
+    d3, p3 = data.reshape(n, k, cs), par.reshape(n, m, cs)
+    stripes = np.concatenate([d3, p3], axis=1)
+    for s in range(n):
+        assert np.array_equal(p3[s], np.stack(O.encode(fam, k, m, list(d3[s]), cs))), s
+    for erased in ([0, 1, 2, 3], [0, 5, 10, 13], [12]):
+        buf = stripes.copy().reshape(-1)
+        buf.reshape(n, k + m, cs)[:, erased] = 0
+        assert O.decode_batch_mt(fam, k, m, cs, buf, n, erased, 4) == 0
+        assert np.array_equal(buf.reshape(n, k + m, cs), stripes), erased
+    buf = stripes.copy().reshape(-1)
+    assert O.decode_batch_mt(fam, k, m, cs, buf, n, [0, 1, 2, 3, 4], 2) != 0  # > m erasures

@@ -145,7 +145,7 @@ int main(int argc, char **argv) {
     const char *co = getenv("MEMEC_GPU_COALESCE");
     printf("{\"bench\": \"coding_adapter\", \"scheme\": \"%s\", \"k\": %u, \"m\": %u, \"chunk\": %u, \"workers\": %d, "
            "\"mode\": \"%s\", \"coalesce\": %s, \"registered\": %d, \"calls_per_s\": %.1f, \"data_GiBps\": %.4f}\n",
-           argv[1], K, M, CS, W, argv[7], co ? co : "256", registered ? 1 : 0, calls / dt, bytes / dt / 1073741824.0);
+           argv[1], K, M, CS, W, argv[7], co ? co : "0", registered ? 1 : 0, calls / dt, bytes / dt / 1073741824.0);
     Coding::destroy(coding);
     return 0;
 }
