@@ -14,7 +14,7 @@ from bench import CONFIGS  # noqa: E402
 from memec_amd import Codec, fill_random  # noqa: E402
 
 
-def run(cfg, rounds=5, wins=(1, 2, 4)):
+def run(cfg, rounds=5, wins=(1, 2, 4), var="MEC_WINDOWS"):
     fam, k, m, cs, n, op, erased = CONFIGS[cfg]
     codec = Codec(fam, k, m, cs, device=0)
     if op == "encode":
@@ -33,7 +33,7 @@ def run(cfg, rounds=5, wins=(1, 2, 4)):
     res = {w: [] for w in wins}
     for _ in range(rounds):
         for w in wins:
-            os.environ["MEC_WINDOWS"] = str(w)
+            os.environ[var] = str(w)
             step()
             ev[0].record()
             for _ in range(10):
@@ -43,13 +43,15 @@ def run(cfg, rounds=5, wins=(1, 2, 4)):
             res[w].append(ev[0].elapsed_time(ev[1]) / 10)
     for w in wins:
         med, best = statistics.median(res[w]), min(res[w])
-        print("%-10s win=%d  median %.4f ms (%.1f%%)  best %.4f ms (%.1f%%)" %
+        print(("%-10s " + var + "=%d  median %.4f ms (%.1f%%)  best %.4f ms (%.1f%%)") %
               (cfg, w, med, nbytes / med / 1e6 / 80, best, nbytes / best / 1e6 / 80), flush=True)
     codec.close()
 
 
 if __name__ == "__main__":
     torch.cuda.set_device(0)
+    var = os.environ.get("AB_VAR", "MEC_WINDOWS")
+    vals = tuple(int(x) for x in os.environ.get("AB_VALUES", "1,2,4").split(","))
     for c in sys.argv[1:] or ["rs_enc", "rs_dec", "rs8_small", "crs_enc", "crs_dec", "rs42"]:
-        run(c)
+        run(c, wins=vals, var=var)
         torch.cuda.empty_cache()
