@@ -159,6 +159,7 @@ def main():
     ap.add_argument("--config", default="rs_enc", choices=sorted(CONFIGS))
     ap.add_argument("--stripes", type=int, default=0, help="override stripes per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the on-box streaming-ceiling measurement (mec_xor)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory (PCIe) batch encode")
     ap.add_argument("--strong", action="store_true",
@@ -235,6 +236,30 @@ def main():
     wall, kern_ms = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize,
                                 dist=dist if world > 1 else None, events=ev)  # one launch per step
 
+    ceiling = None
+    if rank == 0 and not args.no_ceiling:
+        # on-box streaming ceiling: libmec's plain region XOR
+        # (Coding::bitwiseXOR; 2 non-temporal 16-B reads + 1 write per lane,
+        # no arithmetic to speak of) over 3 x 8 GiB, best of 5 — the same
+        # access shape as the coding kernels.  (torch's own copy kernel
+        # reaches only ~4.6-5.0 TB/s here, tools/ceil_probe.py.)
+        from memec_amd import xor as mec_xor
+        a = torch.empty(8 << 30, dtype=torch.uint8, device=dev)
+        b = torch.empty_like(a)
+        out = torch.empty_like(a)
+        mec_xor(out, a, b)
+        best = None
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            mec_xor(out, a, b)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        ceiling = 3 * a.numel() / (best * 1e-3) / 1e9
+        del a, b, out
+
     ok = None
     if op == "decode" and orig is not None:
         ok = bool(torch.equal(stripe[:, erased], orig))
@@ -292,7 +317,9 @@ def main():
                        "op": op, "erased": erased, "parallelism": "stripe-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, stripes),
-                         "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4)},
+                         "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4),
+                         "stream_ceiling_GBps": round(ceiling, 1) if ceiling else None,
+                         "frac_of_stream_ceiling": round(achieved / ceiling, 4) if ceiling else None},
             "cpu_baseline": None,
         }
         if ok is not None:

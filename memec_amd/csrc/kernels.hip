@@ -276,13 +276,15 @@ const auto kGbmTable = make_gbm_table(std::make_index_sequence<8 * kMaxRows>{});
 // ---------------------------------------------------------------------------
 // XOR and fill
 // ---------------------------------------------------------------------------
+// One 16-byte unit per lane over the whole region (grid-stride only past
+// 16 GiB), non-temporal: a plain 2-read / 1-write HBM stream, also the
+// bench's on-box streaming ceiling.  dst may alias a or b (parity ^= delta).
 __global__ __launch_bounds__(kThreads) void xor_kernel(uint8_t *dst, const uint8_t *a, const uint8_t *b,
                                                        uint64_t len) {
     const uint64_t stride = uint64_t(gridDim.x) * kThreads * 16;
     for (uint64_t off = (uint64_t(blockIdx.x) * kThreads + threadIdx.x) * 16; off < len; off += stride) {
         if (off + 16 <= len) {
-            *reinterpret_cast<u32x4 *>(dst + off) =
-                *reinterpret_cast<const u32x4 *>(a + off) ^ *reinterpret_cast<const u32x4 *>(b + off);
+            st_nt<u32x4>(dst + off, ld_nt<u32x4>(a + off) ^ ld_nt<u32x4>(b + off));
         } else {
             const uint32_t n = uint32_t(len - off);
             store_partial(dst + off, load_partial(a + off, n) ^ load_partial(b + off, n), n);
@@ -350,7 +352,9 @@ hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream) {
 
 hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, hipStream_t stream) {
     if (len == 0) return hipSuccess;
-    hipLaunchKernelGGL(xor_kernel, dim3(stream_blocks(len)), dim3(kThreads), 0, stream, dst, a, b, len);
+    const uint64_t units = (len + 15) / 16, blocks = (units + kThreads - 1) / kThreads;
+    hipLaunchKernelGGL(xor_kernel, dim3(uint32_t(std::min<uint64_t>(blocks, uint64_t(1) << 22))), dim3(kThreads), 0,
+                       stream, dst, a, b, len);
     return hipGetLastError();
 }
 
