@@ -35,6 +35,10 @@ CONFIGS = {
     "crs_enc": ("cauchy", 12, 4, 65536, 4096, "encode", None),             # configs[4] per GPU
     "crs_dec": ("cauchy", 12, 4, 65536, 4096, "decode", [0, 1, 2, 3]),
     "rs42": ("rs", 4, 2, 4096, 65536, "encode", None),
+    # the server's delta path (parity_chunk_buffer.cc:342-353): parity ^=
+    # A[:, j] * delta for one data column j (last field = j)
+    "rs8_update": ("rs", 8, 2, 4096, 65536, "update", 3),
+    "rs_update": ("rs", 10, 4, 1 << 20, 4096, "update", 3),
 }
 WORKLOAD_NAMES = {
     "rs_enc": "RS(10,4) encode, 1 MiB chunks, 4096 stripes per GPU (BASELINE configs[1])",
@@ -44,6 +48,8 @@ WORKLOAD_NAMES = {
     "crs_enc": "Cauchy-RS(12,4) encode, 64 KiB chunks, 4096 stripes per GPU (configs[4] sharded)",
     "crs_dec": "Cauchy-RS(12,4) decode {0,1,2,3}, 64 KiB chunks, 4096 stripes per GPU",
     "rs42": "RS(4,2) encode, 4 KiB chunks, 65536 stripes per GPU",
+    "rs8_update": "RS(8,2) delta update of data column 3 into both parities, 4 KiB chunks, 65536 stripes per GPU",
+    "rs_update": "RS(10,4) delta update of data column 3 into all 4 parities, 1 MiB chunks, 4096 stripes per GPU",
 }
 
 
@@ -122,6 +128,39 @@ def cpu_baseline_decode(fam, k, m, cs, erased, codewords, threads):
                       % (sample, passes, erased, threads),
             "single_thread_value": round(single, 4),
             "matches_gpu": bool(rc == 0 and np.array_equal(view, codewords)), "cpu_model": cpu_model()}
+
+
+def cpu_baseline_update(fam, k, m, cs, j, threads):
+    """The reference's delta path on the CPU: Coding::encode over the k
+    columns with Coding::zeros everywhere but column j (the plugin reads and
+    multiplies the zero chunks too, rscoding.cc:51-95), then
+    Coding::bitwiseXOR of the result into the parity (coding.cc:88-118,
+    parity_chunk_buffer.cc:387-393); threads on disjoint stripes."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import _oracle as O
+
+    sample = max(threads, min(256, (768 << 20) // ((k + 2 * m) * cs)))
+    sample = (sample // threads) * threads or threads
+    data = np.zeros((sample, k, cs), np.uint8)
+    data[:, j] = O.fill(sample * cs, 5).reshape(sample, cs)
+    data = data.reshape(-1)
+    delta_par = np.zeros(sample * m * cs, np.uint8)
+    parity = O.fill(sample * m * cs, 6)
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        O.encode_batch_mt(fam, k, m, cs, data, delta_par, sample, threads)
+        np.bitwise_xor(parity, delta_par, out=parity)
+        passes += 1
+        t_total = time.perf_counter() - t0
+        if t_total * threads >= 10.0 or passes >= 64:
+            break
+    value = passes * sample * cs / t_total / 2**30
+    return {"value": round(value, 4), "unit": "GiB/s (delta bytes)", "cores": threads, "kind": "port",
+            "sample": "%d stripes x %d passes: orc_encode_batch_mt over the zero-padded delta stripe + XOR "
+                      "into parity (numpy), %d threads" % (sample, passes, threads),
+            "matches_gpu": None, "cpu_model": cpu_model()}
 
 
 def cpu_model():
@@ -205,6 +244,18 @@ def main():
         def step():
             codec.encode(data, parity)
         alg_bytes = (k + m) * cs * stripes
+    elif op == "update":
+        j = erased  # the updated data column
+        erased = None
+        delta = torch.empty(stripes, cs, dtype=torch.uint8, device=dev)
+        fill_random(delta, seed + 1)
+        parity = torch.zeros(stripes, m, cs, dtype=torch.uint8, device=dev)  # parity of all-zero data
+        n_updates = [0]
+
+        def step():
+            codec.encode_update(j, delta, parity)
+            n_updates[0] += 1
+        alg_bytes = (1 + 2 * m) * cs * stripes  # read delta, read + write every parity
     else:
         stripe = torch.empty(stripes, k + m, cs, dtype=torch.uint8, device=dev)
         d = torch.empty(stripes, k, cs, dtype=torch.uint8, device=dev)
@@ -263,6 +314,18 @@ def main():
     ok = None
     if op == "decode" and orig is not None:
         ok = bool(torch.equal(stripe[:, erased], orig))
+    if op == "update":
+        # parity started as the parity of all-zero data and received the
+        # same delta n times: it must equal the encode of (delta in column
+        # j, zeros elsewhere) if n is odd, zero if n is even
+        ref = torch.zeros(min(stripes, 256), m, cs, dtype=torch.uint8, device=dev)
+        if n_updates[0] % 2:
+            dz = torch.zeros(ref.shape[0], k, cs, dtype=torch.uint8, device=dev)
+            dz[:, j] = delta[:ref.shape[0]]
+            codec.encode(dz, ref)
+            del dz
+        ok = bool(torch.equal(parity[:ref.shape[0]], ref))
+        del ref
 
     gpu_parity_np = None
     if rank == 0 and op == "encode" and not args.no_cpu_baseline:
@@ -297,7 +360,9 @@ def main():
                **res}
 
     if rank == 0:
-        value = global_stripes * k * cs * args.steps / wall / 2**30
+        # data GiB/s: k data chunks per stripe (encode / decode), the one
+        # delta chunk per stripe for updates
+        value = global_stripes * (cs if op == "update" else k * cs) * args.steps / wall / 2**30
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         line = {
             "metric": METRIC,
@@ -323,7 +388,7 @@ def main():
             "cpu_baseline": None,
         }
         if ok is not None:
-            line["decode_verified"] = ok
+            line["decode_verified" if op == "decode" else "update_verified"] = ok
         if e2e:
             line["e2e_host_memory"] = e2e
         if not args.no_cpu_baseline and world == 1:
@@ -331,6 +396,8 @@ def main():
             try:
                 if op == "encode":
                     line["cpu_baseline"] = cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads)
+                elif op == "update":
+                    line["cpu_baseline"] = cpu_baseline_update(fam, k, m, cs, j, threads)
                 else:
                     line["cpu_baseline"] = cpu_baseline_decode(fam, k, m, cs, erased, codewords_np, threads)
             except Exception as exc:  # report, never fake

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
 #pragma unroll
         for (int i = 0; i < R; ++i)
 #pragma unroll
-            for (int l = 0; l < W; ++l) acc[i * W + l] = p.accumulate ? buf_ld<vec>(dr[i], off + l * pk, false) : vec(0);
+            for (int l = 0; l < W; ++l) acc[i * W + l] = p.accumulate ? buf_ld<vec>(dr[i], off + l * pk, true) : vec(0);
         {
             const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(srow[p.src_off[0]], p.chunk);
 #pragma unroll
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
             for (int i = 0; i < R; ++i)
 #pragma unroll
                 for (int l = 0; l < W; ++l)
-                    acc[i * W + l] = *reinterpret_cast<const vec *>(db + p.dst_off[i] + uint64_t(l) * p.packet);
+                    acc[i * W + l] = ld_nt<vec>(db + p.dst_off[i] + uint64_t(l) * p.packet);
         } else {
 #pragma unroll
             for (int r = 0; r < ROWS; ++r) acc[r] = vec(0);

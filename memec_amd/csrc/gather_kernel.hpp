@@ -99,7 +99,7 @@ __global__ __launch_bounds__(kThreads) void gf8_gather_kernel(const GatherParams
     for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(uniform64(ptr[K + i]), p.chunk);
     u32x4 acc[R];
 #pragma unroll
-    for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, false) : u32x4{0, 0, 0, 0};
+    for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
     gf8_apply<K, R, kGf8Dense>(d, acc, dsc + kGf8DescHead + opaque_zero());
 #pragma unroll
     for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(kThreads) void bm_gather_kernel(const GatherParams 
 #pragma unroll
     for (int i = 0; i < R; ++i)
 #pragma unroll
-        for (int l = 0; l < W; ++l) acc[i * W + l] = p.accumulate ? buf_ld<vec>(dr[i], off + l * pk, false) : vec(0);
+        for (int l = 0; l < W; ++l) acc[i * W + l] = p.accumulate ? buf_ld<vec>(dr[i], off + l * pk, true) : vec(0);
     vec d[W], nx[W];
     {
         const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(uniform64(ptr[0]), p.chunk);

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
 #pragma unroll
         for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(drow[p.dst_off[i]], p.chunk);
 #pragma unroll
-        for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, false) : u32x4{0, 0, 0, 0};
+        for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
         gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
 #pragma unroll
         for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
@@ -175,9 +175,10 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
         uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
 #pragma unroll
         for (int j = 0; j < K; ++j) d[j] = ld_nt<u32x4>(sb + p.src_off[j]);
-        if (p.accumulate) {
+        if (p.accumulate) {  // read-modify-write of the outputs, streamed too
+                             // (non-temporal: RS(10,4) update 70.9 -> 73.9 %)
 #pragma unroll
-            for (int i = 0; i < R; ++i) acc[i] = *reinterpret_cast<const u32x4 *>(db + p.dst_off[i]);
+            for (int i = 0; i < R; ++i) acc[i] = ld_nt<u32x4>(db + p.dst_off[i]);
         } else {
 #pragma unroll
             for (int i = 0; i < R; ++i) acc[i] = u32x4{0, 0, 0, 0};

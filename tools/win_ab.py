@@ -23,6 +23,12 @@ def run(cfg, rounds=5, wins=(1, 2, 4), var="MEC_WINDOWS"):
         par = torch.empty(n, m, cs, dtype=torch.uint8, device="cuda")
         step = lambda: codec.encode(data, par)  # noqa: E731
         nbytes = (k + m) * cs * n
+    elif op == "update":
+        delta = torch.empty(n, cs, dtype=torch.uint8, device="cuda")
+        fill_random(delta, 1)
+        par = torch.zeros(n, m, cs, dtype=torch.uint8, device="cuda")
+        step = lambda: codec.encode_update(erased, delta, par)  # noqa: E731
+        nbytes = (1 + 2 * m) * cs * n
     else:
         st = torch.empty(n, k + m, cs, dtype=torch.uint8, device="cuda")
         fill_random(st, 1)
