@@ -37,6 +37,10 @@
  *                                server's delta encodes
  *                                (parity_chunk_buffer.cc:342-353,
  *                                degraded_chunk_buffer.cc:645-656)
+ *   mec_create_multi             one server process driving several GPUs: its
+ *                                host-memory calls spread over them (SURVEY
+ *                                §8e; the reference has no GPU, one Coding
+ *                                per server process, server.cc:107)
  *   mec_set_coalescing           batching of concurrent mec_*_host calls from
  *                                the server's worker threads, which share one
  *                                Coding instance (server.cc:107,
@@ -146,6 +150,19 @@ int mec_encode(mec_ctx *ctx,
                const uint8_t *data, int64_t data_stripe_stride, int64_t data_chunk_stride,
                uint8_t *parity, int64_t parity_stripe_stride, int64_t parity_chunk_stride,
                uint32_t n_stripes, uint32_t parity_mask, void *stream);
+
+/* Multi-GPU context for one host process (MemEC runs one server process
+ * per node, chunks in host memory).  devices[0..n_devices-1] are HIP
+ * ordinals (a device may repeat).  Host-memory batches (mec_encode_batch /
+ * mec_decode_batch / mec_encode_update_batch with MEC_MEM_HOST,
+ * mec_encode_host_batch) are cut into contiguous stripe ranges, one per
+ * device ([g*N/G, (g+1)*N/G)), and run concurrently, each GPU over its own
+ * PCIe link; single-stripe host calls go to the devices round-robin;
+ * device-memory calls run on devices[0].  No data moves between GPUs
+ * (stripes are independent).  mec_get_stats sums the devices; destroy with
+ * mec_destroy. */
+int mec_create_multi(int family, uint32_t k, uint32_t m, uint32_t chunk_size,
+                     const int *devices, uint32_t n_devices, mec_ctx **out);
 
 /* Decode n_stripes stripes in place.  chunks holds all k+m chunks of every
  * stripe (strided).  Bit i of present_mask set <=> chunk i is present

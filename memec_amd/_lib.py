@@ -15,7 +15,7 @@ FAMILIES = {"rs": 0, "cauchy": 1, "isal_rs": 2, "isal_cauchy": 3}
 
 # Exported symbols declared by include/mec.h (checked by tests/test_abi.py).
 SYMBOLS = (
-    "mec_abi_version", "mec_create", "mec_destroy", "mec_last_error", "mec_get_info",
+    "mec_abi_version", "mec_create", "mec_create_multi", "mec_destroy", "mec_last_error", "mec_get_info",
     "mec_get_matrix", "mec_get_bitmatrix", "mec_encode", "mec_decode", "mec_decode_split",
     "mec_encode_update", "mec_xor", "mec_fill_random", "mec_encode_host", "mec_decode_host",
     "mec_encode_update_host", "mec_encode_host_batch", "mec_host_register", "mec_host_unregister",
@@ -60,6 +60,8 @@ def lib():
     L = ctypes.CDLL(LIB_PATH)
     L.mec_last_error.restype = ctypes.c_char_p
     L.mec_create.argtypes = [ctypes.c_int, u32, u32, u32, ctypes.c_int, ctypes.POINTER(vp)]
+    L.mec_create_multi.argtypes = [ctypes.c_int, u32, u32, u32, ctypes.POINTER(ctypes.c_int), u32,
+                                   ctypes.POINTER(vp)]
     L.mec_destroy.argtypes = [vp]
     L.mec_destroy.restype = None
     L.mec_get_info.argtypes = [vp, ctypes.POINTER(MecInfo)]

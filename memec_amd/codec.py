@@ -34,10 +34,16 @@ class Codec:
 
     device=-1 makes a host-only context (matrices only; compute raises)."""
 
-    def __init__(self, family, k, m, chunk_size, device=0):
+    def __init__(self, family, k, m, chunk_size, device=0, devices=None):
+        """devices: list of GPU ordinals -> a multi-GPU context (host-memory
+        batches split over them, include/mec.h mec_create_multi)."""
         self._h = vp()
         fam = _lib.FAMILIES[family] if isinstance(family, str) else int(family)
-        check(lib().mec_create(fam, k, m, chunk_size, device, ctypes.byref(self._h)))
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            check(lib().mec_create_multi(fam, k, m, chunk_size, arr, len(devices), ctypes.byref(self._h)))
+        else:
+            check(lib().mec_create(fam, k, m, chunk_size, device, ctypes.byref(self._h)))
         inf = _lib.MecInfo()
         check(lib().mec_get_info(self._h, ctypes.byref(inf)))
         self.family, self.k, self.m, self.w = family, inf.k, inf.m, inf.w

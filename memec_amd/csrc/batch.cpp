@@ -682,6 +682,11 @@ int mec_encode_batch(mec_ctx *c, const uint8_t *const *data, uint8_t *const *par
     if (mem_kind != MEC_MEM_DEVICE && mem_kind != MEC_MEM_HOST) return fail(MEC_EINVAL, "bad mem_kind %d", mem_kind);
     if (n_stripes == 0) return MEC_OK;
     if (!data || !parity) return fail(MEC_EINVAL, "null pointer array");
+    if (mem_kind == MEC_MEM_HOST && is_multi(c))
+        return shard_run(c, n_stripes, [&](mec_ctx *sc, uint32_t s0, uint32_t s1) {
+            return mec_encode_batch(sc, data + size_t(s0) * c->k, parity + size_t(s0) * c->m, s1 - s0, parity_mask,
+                                    MEC_MEM_HOST, nullptr);
+        });
     const uint32_t pm = parity_mask ? parity_mask : full_mask32(c->m);
     DeviceGuard dg(c->device);
     if (mem_kind == MEC_MEM_DEVICE) {
@@ -706,6 +711,41 @@ int mec_decode_batch(mec_ctx *c, uint8_t *const *chunks, const uint64_t *present
     if (mem_kind != MEC_MEM_DEVICE && mem_kind != MEC_MEM_HOST) return fail(MEC_EINVAL, "bad mem_kind %d", mem_kind);
     if (n_stripes == 0) return MEC_OK;
     if (!chunks || !present_masks) return fail(MEC_EINVAL, "null pointer array");
+    if (mem_kind == MEC_MEM_HOST && is_multi(c)) {
+        // every shard reports its stripes' results; like one context, the
+        // call returns the first failing stripe's status (with its text)
+        std::vector<int32_t> res(n_stripes, MEC_OK);
+        const size_t row = size_t(c->k) + c->m;
+        std::mutex emu;
+        std::vector<std::pair<uint32_t, std::string>> errs;  // (first stripe of the shard, its error)
+        const int rc = shard_run(c, n_stripes, [&](mec_ctx *sc, uint32_t s0, uint32_t s1) -> int {
+            const int r = mec_decode_batch(sc, chunks + s0 * row, present_masks + s0, s1 - s0, res.data() + s0,
+                                           MEC_MEM_HOST, nullptr);
+            if (r == MEC_OK) return MEC_OK;
+            bool per_stripe = false;
+            for (uint32_t s = s0; s < s1 && !per_stripe; ++s) per_stripe = res[s] == r;
+            if (!per_stripe) return r;  // not attributable to a stripe: a real failure
+            std::lock_guard<std::mutex> lk(emu);
+            errs.emplace_back(s0, g_err);
+            return MEC_OK;
+        });
+        if (results) std::copy(res.begin(), res.end(), results);
+        if (rc != MEC_OK) return rc;
+        for (uint32_t s = 0; s < n_stripes; ++s)
+            if (res[s] != MEC_OK) {
+                std::string text;
+                uint32_t best = 0;
+                for (const auto &e : errs)
+                    if (e.first <= s && e.first >= best) {
+                        best = e.first;
+                        text = e.second;
+                    }
+                // the shard numbers its stripes from its range start
+                g_err = "shard starting at stripe " + std::to_string(best) + ": " + text;
+                return res[s];
+            }
+        return MEC_OK;
+    }
     int first = MEC_OK;
     std::string first_err;
     const uint32_t n = c->k + c->m;
@@ -787,6 +827,11 @@ int mec_encode_update_batch(mec_ctx *c, const uint32_t *data_index, const uint8_
     if (!data_index || !delta || !parity) return fail(MEC_EINVAL, "null pointer array");
     for (uint32_t s = 0; s < n_stripes; ++s)
         if (data_index[s] >= c->k) return fail(MEC_EINVAL, "stripe %u: data_index %u >= k %u", s, data_index[s], c->k);
+    if (mem_kind == MEC_MEM_HOST && is_multi(c))
+        return shard_run(c, n_stripes, [&](mec_ctx *sc, uint32_t s0, uint32_t s1) {
+            return mec_encode_update_batch(sc, data_index + s0, delta + s0, parity + size_t(s0) * c->m, s1 - s0,
+                                           parity_mask, MEC_MEM_HOST, nullptr);
+        });
     const uint32_t pm = parity_mask ? parity_mask : full_mask32(c->m);
     DeviceGuard dg(c->device);
     if (mem_kind == MEC_MEM_DEVICE) {
@@ -820,6 +865,7 @@ int mec_encode_update_batch(mec_ctx *c, const uint32_t *data_index, const uint8_
 
 int mec_set_coalescing(mec_ctx *c, uint32_t max_batch) {
     CHECK_CTX(c);
+    for (mec_ctx *sc : c->shards) (void)mec_set_coalescing(sc, max_batch);
     std::lock_guard<std::mutex> lk(c->coal.mu);
     c->coal.max_batch = max_batch;
     return MEC_OK;
@@ -836,6 +882,15 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
     {
         std::lock_guard<std::mutex> pk(c->plan_mu);
         out->cached_plans = c->plans.size();
+    }
+    for (mec_ctx *sc : c->shards) {  // a multi context reports its shards' sums
+        mec_stats t{};
+        (void)mec_get_stats(sc, &t);
+        out->coalesced_batches += t.coalesced_batches;
+        out->coalesced_requests += t.coalesced_requests;
+        out->cached_plans += t.cached_plans;
+        out->zero_copy_calls += t.zero_copy_calls;
+        out->staged_calls += t.staged_calls;
     }
     return MEC_OK;
 }

@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -126,6 +127,9 @@ struct mec_ctx {
     mec::core::HostPipe pipe;
     mec::core::Coalescer coal;
     std::atomic<uint64_t> zc_calls{0}, staged_calls{0};  // host-call statistics
+    // multi-GPU context (multi.cpp): one ordinary context per device
+    std::vector<mec_ctx *> shards;
+    std::atomic<uint32_t> rr{0};
 
     bool byte_wise() const { return family != MEC_CAUCHY_GOOD; }
     mec::Scheme scheme() const {
@@ -203,6 +207,13 @@ struct LaneHold {
 bool zc_device_address(const void *p, size_t len, uint64_t &dev);
 bool zc_any_registered();
 bool zc_translate(uint64_t *ptrs, size_t n, size_t len);
+
+// multi.cpp: multi-GPU contexts.  shard_run runs fn(shard, s0, s1) on every
+// shard's contiguous stripe range concurrently and returns the first error
+// (its text prefixed with the device); shard_pick round-robins.
+bool is_multi(const mec_ctx *c);
+mec_ctx *shard_pick(mec_ctx *c);
+int shard_run(mec_ctx *c, uint32_t n, const std::function<int(mec_ctx *, uint32_t, uint32_t)> &fn);
 
 // batch.cpp
 void batch_release(mec_ctx *c);  // frees table slots and the host pipeline

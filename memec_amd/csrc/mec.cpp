@@ -276,6 +276,8 @@ int mec_create(int family, uint32_t k, uint32_t m, uint32_t chunk_size, int devi
 
 void mec_destroy(mec_ctx *c) {
     if (!c) return;
+    for (mec_ctx *s : c->shards) mec_destroy(s);
+    c->shards.clear();
     if (has_device(c)) {
         DeviceGuard g(c->device);
         batch_release(c);
@@ -396,6 +398,7 @@ int mec_fill_random(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_off
 
 int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *parity) {
     CHECK_CTX(c);
+    if (is_multi(c)) return mec_encode_host(shard_pick(c), data, parity);
     if (!data || !parity) return fail(MEC_EINVAL, "null pointer array");
     std::vector<uint32_t> rows, cols;
     for (uint32_t i = 0; i < c->m; ++i)
@@ -440,6 +443,7 @@ int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *pari
 
 int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
     CHECK_CTX(c);
+    if (is_multi(c)) return mec_decode_host(shard_pick(c), chunks, present_mask);
     if (!chunks) return fail(MEC_EINVAL, "null pointer array");
     std::shared_ptr<mec::LinearPlan> plan;
     int rc = get_plan(c, present_mask, plan);
@@ -477,6 +481,7 @@ int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
 
 int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta, uint8_t *const *parity) {
     CHECK_CTX(c);
+    if (is_multi(c)) return mec_encode_update_host(shard_pick(c), data_index, delta, parity);
     if (!delta || !parity) return fail(MEC_EINVAL, "null pointer");
     if (data_index >= c->k) return fail(MEC_EINVAL, "data_index %u >= k %u", data_index, c->k);
     std::vector<uint32_t> rows, cols{data_index};
@@ -514,6 +519,12 @@ int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint
                           uint32_t parity_mask) {
     CHECK_CTX(c);
     if (!data || !parity) return fail(MEC_EINVAL, "null buffer");
+    if (is_multi(c)) {
+        const size_t dbytes = size_t(c->k) * c->cs, pbytes = size_t(c->m) * c->cs;
+        return shard_run(c, n_stripes, [&](mec_ctx *sc, uint32_t s0, uint32_t s1) {
+            return mec_encode_host_batch(sc, data + s0 * dbytes, parity + s0 * pbytes, s1 - s0, parity_mask);
+        });
+    }
     DeviceGuard dg(c->device);
     std::lock_guard<std::mutex> bg(c->batch_mu);
     const size_t cs = c->cs, dbytes = size_t(c->k) * cs, pbytes = size_t(c->m) * cs;
