@@ -9,6 +9,22 @@ static int adapter_device() {
     return e ? atoi(e) : 0;
 }
 
+// MEMEC_GPU_DEVICES=0,1,2,3: one server process drives several GPUs
+// (mec_create_multi: host-memory calls spread over them); empty = one
+// device (MEMEC_GPU_DEVICE).
+static int adapter_devices(int *out, int cap) {
+    const char *e = getenv("MEMEC_GPU_DEVICES");
+    int n = 0;
+    while (e && *e && n < cap) {
+        char *end = 0;
+        const long v = strtol(e, &end, 10);
+        if (end == e) break;
+        out[n++] = int(v);
+        e = *end == ',' ? end + 1 : end;
+    }
+    return n;
+}
+
 // One instance is shared by every server worker thread (server.cc:107,
 // worker.cc:128-137), each issuing single-stripe calls.  Each call is one
 // launch on the calling thread's own stream, coding the chunks in place
@@ -25,7 +41,10 @@ GpuMatrixCoding::GpuMatrixCoding(int family, const char *name, uint32_t k, uint3
     : _name(name), _family(family), _k(k), _m(m), _chunkSize(chunkSize), _ctx(0) {
     // Parameter errors exit(-1) with a message, like rscoding.cc:26-29 and
     // rscoding.cc:205-213 / cauchycoding.cc:193-196.
-    int rc = mec_create(family, k, m, chunkSize, adapter_device(), &_ctx);
+    int devs[64];
+    const int nd = adapter_devices(devs, 64);
+    int rc = nd > 0 ? mec_create_multi(family, k, m, chunkSize, devs, uint32_t(nd), &_ctx)
+                    : mec_create(family, k, m, chunkSize, adapter_device(), &_ctx);
     if (rc != MEC_OK) {
         fprintf(stderr, "%s: %s\n", _name, mec_last_error());
         exit(-1);
