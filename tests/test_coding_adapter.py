@@ -45,3 +45,17 @@ def test_coding_flow_on_gpu(binaries, args):
         r = subprocess.run([b] + args, capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, (b, args, r.stdout, r.stderr)
         assert ": ok" in r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"MEMEC_GPU_DEVICES": "0,0"}, {"MEMEC_GPU_COALESCE": "64"}])
+def test_coding_flow_adapter_modes(binaries, env):
+    """The same flow with the adapter driving a multi-device context
+    (MEMEC_GPU_DEVICES, device repeated on a one-GPU box) and with the
+    request coalescer on."""
+    for b in binaries:
+        for args in (["rs", "10", "4", "65536"], ["cauchy", "12", "4", "65536"]):
+            r = subprocess.run([b] + args, capture_output=True, text=True, timeout=120,
+                               env=dict(os.environ, **env))
+            assert r.returncode == 0, (b, args, env, r.stdout, r.stderr)
+            assert ": ok" in r.stdout
