@@ -15,6 +15,7 @@
 // loads, uniform per block).  Decode plans are cached per pattern, so a
 // batch of mixed erasures costs one host-side plan per distinct pattern
 // (the reference rebuilds matrices per call, jerasure.c:223, 958).
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -376,11 +377,18 @@ struct Copy {
     const void *src;
 };
 
+// Threads for packing / unpacking staged chunks (MEC_COPY_THREADS, default 8).
+unsigned copy_threads() {
+    const char *e = std::getenv("MEC_COPY_THREADS");
+    const int v = e ? std::atoi(e) : 8;
+    return unsigned(std::max(1, std::min(v, 64)));
+}
+
 // memcpy of many equal-sized chunks, split over a few threads when large.
 void copy_chunks(const std::vector<Copy> &ops, size_t len) {
     const size_t bytes = ops.size() * len;
     unsigned nt = 1;
-    if (bytes >= (size_t(8) << 20)) nt = std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency() / 2));
+    if (bytes >= (size_t(8) << 20)) nt = std::min<unsigned>(copy_threads(), std::max(1u, std::thread::hardware_concurrency() / 2));
     nt = std::min<unsigned>(nt, unsigned(ops.size()));
     auto work = [&](unsigned t) {
         const size_t a = ops.size() * t / nt, b = ops.size() * (t + 1) / nt;
