@@ -214,9 +214,12 @@ size_t build_descs(const mec_ctx *c, const MapSet &M, std::vector<uint32_t> &out
     return groups;
 }
 
-// Pinned + device staging of one call's tables, reused round-robin.
+// Pinned + device staging of one call's tables, reused round-robin.  With
+// `mapped` the kernels read the tables in place from the pinned buffer (no
+// copy; small zero-copy batches, where the copy would be most of the call)
+// and `base` is its device address; otherwise `base` is the HBM copy.
 int table_upload(mec_ctx *c, const std::vector<std::pair<const void *, size_t>> &parts, TableSlot *&slot,
-                 std::vector<size_t> &offs, hipStream_t st) {
+                 std::vector<size_t> &offs, hipStream_t st, bool mapped, uint8_t *&base) {
     size_t total = 0;
     offs.clear();
     for (const auto &pr : parts) {
@@ -239,18 +242,24 @@ int table_upload(mec_ctx *c, const std::vector<std::pair<const void *, size_t>> 
     if (t.cap < total) {
         if (t.host) (void)hipHostFree(t.host);
         if (t.dev) (void)hipFree(t.dev);
-        t.host = nullptr;
+        t.host = t.hdev = nullptr;
         t.dev = nullptr;
         t.cap = 0;
         const size_t cap = std::max<size_t>(total, size_t(1) << 20);
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.host), cap, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&t.host), cap, hipHostMallocMapped));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&t.hdev), t.host, 0));
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&t.dev), cap));
         t.cap = cap;
     }
     uint8_t *h = reinterpret_cast<uint8_t *>(t.host);
     for (size_t i = 0; i < parts.size(); ++i)
         if (parts[i].second) std::memcpy(h + offs[i], parts[i].first, parts[i].second);
+    if (mapped) {
+        base = reinterpret_cast<uint8_t *>(t.hdev);
+        return MEC_OK;
+    }
     HIP_TRY(hipMemcpyAsync(t.dev, t.host, total, hipMemcpyHostToDevice, st));
+    base = reinterpret_cast<uint8_t *>(t.dev);
     return MEC_OK;
 }
 
@@ -268,7 +277,7 @@ struct SlotHold {
 // stab / dtab: host arrays of n rows of device chunk pointers; pat: per-stripe
 // map index (nullptr = map 0).
 int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, const void *dtab, uint32_t dstride,
-               const uint16_t *pat, uint32_t n, hipStream_t st) {
+               const uint16_t *pat, uint32_t n, hipStream_t st, bool mapped_tables = false) {
     if (M.ssel.empty() || M.rows() == 0 || n == 0) return MEC_OK;
     // a single map with no skipped stripe runs from kernel arguments;
     // anything else through per-stripe descriptors
@@ -287,9 +296,9 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
     SlotHold hold;
     hold.st = st;
     std::vector<size_t> offs;
-    int rc = table_upload(c, parts, hold.t, offs, st);
+    uint8_t *dev = nullptr;
+    int rc = table_upload(c, parts, hold.t, offs, st, mapped_tables, dev);
     if (rc != MEC_OK) return rc;
-    uint8_t *dev = reinterpret_cast<uint8_t *>(hold.t->dev);
     const uint64_t *dstab = reinterpret_cast<const uint64_t *>(dev + offs[0]);
     const uint64_t *ddtab = reinterpret_cast<const uint64_t *>(dev + offs[same ? 0 : 1]);
     const size_t rows = M.rows(), nm = M.ssel.size();
@@ -462,7 +471,9 @@ int run_zerocopy(mec_ctx *c, std::vector<Group> &gs) {
         for (uint32_t j = 0; j < g.ns; ++j) ss[j] = uint8_t(j);
         for (uint32_t i = 0; i < g.nd; ++i) ds[i] = uint8_t(g.ns + i);
         M.add(ss, ds, g.coef);
-        rc = run_gather(c, M, rows[q].data(), row, rows[q].data(), row, nullptr, g.n, h.l->stream);
+        // small batches (coalesced single-stripe calls) read their pointer
+        // rows in place from pinned memory: one launch, no table copy
+        rc = run_gather(c, M, rows[q].data(), row, rows[q].data(), row, nullptr, g.n, h.l->stream, g.n <= 256);
     }
     // no launch may outlive the call (the caller owns the chunks)
     hipError_t e = hipStreamSynchronize(h.l->stream);
@@ -609,17 +620,18 @@ void execute(mec_ctx *c, std::vector<Request *> &batch) {
     c->coal.requests += batch.size();
 }
 
-// Leader/follower group commit: the first caller to find no batch in
-// flight takes everything queued (up to max_batch) and runs it; callers
-// arriving meanwhile queue up for the next batch, so the batch size grows
-// with the offered load and an idle system pays no wait.
+// Leader/follower group commit: a caller that finds fewer than kMaxLeaders
+// batches in flight takes everything queued (up to max_batch) and runs it;
+// callers arriving meanwhile queue up for the next batch, so the batch size
+// grows with the offered load and an idle system pays no wait.  Several
+// batches in flight keep the GPU and the host copies overlapped.
 int submit(mec_ctx *c, Request &req) {
     Coalescer &C = c->coal;
     std::unique_lock<std::mutex> lk(C.mu);
     C.queue.push_back(&req);
     while (!req.done) {
-        if (!C.leader_active) {
-            C.leader_active = true;
+        if (C.leaders < kMaxLeaders && !C.queue.empty()) {
+            ++C.leaders;
             std::vector<Request *> batch;
             const uint32_t cap = std::max<uint32_t>(1, C.max_batch);
             while (!C.queue.empty() && batch.size() < cap) {
@@ -630,7 +642,7 @@ int submit(mec_ctx *c, Request &req) {
             execute(c, batch);
             lk.lock();
             for (Request *r : batch) r->done = true;
-            C.leader_active = false;
+            --C.leaders;
             C.cv.notify_all();
         } else {
             C.cv.wait(lk);

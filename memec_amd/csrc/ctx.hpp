@@ -69,7 +69,8 @@ struct Lane {
 // launch that reads it; the slot is reused only after it fired.
 struct TableSlot {
     std::mutex mu;
-    uint64_t *host = nullptr;
+    uint64_t *host = nullptr;  // pinned + GPU-mapped
+    uint64_t *hdev = nullptr;  // device address of host (small zero-copy batches read it in place)
     uint64_t *dev = nullptr;
     size_t cap = 0;  // entries
     hipEvent_t done = nullptr;
@@ -93,11 +94,13 @@ struct HostPipe {
 // One pending single-stripe host request (mec_*_host while coalescing).
 struct Request;
 
+constexpr uint32_t kMaxLeaders = 4;
+
 struct Coalescer {
     std::mutex mu;
     std::condition_variable cv;
     std::deque<Request *> queue;
-    bool leader_active = false;
+    uint32_t leaders = 0;    // batches in flight (at most kMaxLeaders)
     uint32_t max_batch = 0;  // 0 = coalescing off
     uint64_t batches = 0, requests = 0;  // statistics
 };

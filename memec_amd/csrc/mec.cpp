@@ -406,6 +406,8 @@ int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *pari
     if (rows.empty()) return MEC_OK;
     for (uint32_t j = 0; j < c->k; ++j)
         if (data[j]) cols.push_back(j);
+    // concurrent calls batched into one launch (mec_set_coalescing)
+    if (coalescing(c)) return submit_encode(c, data, parity);
     {
         std::vector<const uint8_t *> zs;
         std::vector<uint8_t *> zo;
@@ -415,9 +417,6 @@ int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *pari
         int zrc = zc_single(c, zs, zo, encode_rows(c, rows, cols), false, taken);
         if (taken) return zrc;
     }
-    // staged calls are worth coalescing (one PCIe round trip per batch);
-    // zero-copy calls are not (they run concurrently on lane streams)
-    if (coalescing(c)) return submit_encode(c, data, parity);
     c->staged_calls++;
     DeviceGuard dg(c->device);
     int rc = MEC_OK;
@@ -451,6 +450,7 @@ int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
     if (plan->dst.empty()) return MEC_OK;
     for (uint32_t i = 0; i < c->k + c->m; ++i)
         if (!chunks[i]) return fail(MEC_EINVAL, "chunk %u pointer is NULL", i);
+    if (coalescing(c)) return submit_decode(c, chunks, present_mask);
     {
         std::vector<const uint8_t *> zs;
         std::vector<uint8_t *> zo;
@@ -460,7 +460,6 @@ int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
         int zrc = zc_single(c, zs, zo, plan->coef, false, taken);
         if (taken) return zrc;
     }
-    if (coalescing(c)) return submit_decode(c, chunks, present_mask);
     c->staged_calls++;
     DeviceGuard dg(c->device);
     LaneHold h{c, lane_acquire(c, rc)};
@@ -488,6 +487,7 @@ int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta
     for (uint32_t i = 0; i < c->m; ++i)
         if (parity[i]) rows.push_back(i);
     if (rows.empty()) return MEC_OK;
+    if (coalescing(c)) return submit_update(c, data_index, delta, parity);
     {
         std::vector<uint8_t *> zo;
         for (uint32_t i : rows) zo.push_back(parity[i]);
@@ -495,7 +495,6 @@ int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta
         int zrc = zc_single(c, {delta}, zo, encode_rows(c, rows, cols), true, taken);
         if (taken) return zrc;
     }
-    if (coalescing(c)) return submit_update(c, data_index, delta, parity);
     c->staged_calls++;
     DeviceGuard dg(c->device);
     int rc = MEC_OK;
