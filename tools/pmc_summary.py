@@ -19,16 +19,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def per_launch(path, counter):
-    vals, names = [], set()
+    """Average per launch of the dominant coding kernel (the one launched
+    most often: the timed step), ignoring setup / verification launches."""
+    by_name = {}
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row["Kernel_Name"]
             if row["Counter_Name"] != counter:
                 continue
             if "gf8_kernel" in name or "bm_kernel" in name:
-                vals.append(float(row["Counter_Value"]))
-                names.add(name)
-    return (sum(vals) / len(vals) if vals else None), len(vals), sorted(names)
+                by_name.setdefault(name, []).append(float(row["Counter_Value"]))
+    if not by_name:
+        return None, 0, []
+    name = max(by_name, key=lambda n: len(by_name[n]))
+    vals = by_name[name]
+    return sum(vals) / len(vals), len(vals), [name]
 
 
 def main(cfgs, out_dir, tag):
@@ -44,8 +49,12 @@ def main(cfgs, out_dir, tag):
         fetch_kib, nf, names = per_launch(fpath, "FETCH_SIZE")
         write_kib, nw, _ = per_launch(wpath, "WRITE_SIZE")
         fam, k, m, cs, stripes, op, erased = CONFIGS[cfg]
-        read_alg = (k * cs * stripes)
-        write_alg = (m if op == "encode" else len(erased)) * cs * stripes
+        if op == "update":  # read delta + m parities, write m parities
+            read_alg = (1 + m) * cs * stripes
+            write_alg = m * cs * stripes
+        else:
+            read_alg = (k * cs * stripes)
+            write_alg = (m if op == "encode" else len(erased)) * cs * stripes
         rd = 2 * fetch_kib * 1024
         wr = write_kib * 1024
         rec = {"config": cfg, "kernels": names, "launches": [nf, nw],
