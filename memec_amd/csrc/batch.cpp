@@ -476,7 +476,7 @@ int run_zerocopy(mec_ctx *c, std::vector<Group> &gs) {
         rc = run_gather(c, M, rows[q].data(), row, rows[q].data(), row, nullptr, g.n, h.l->stream, g.n <= 256);
     }
     // no launch may outlive the call (the caller owns the chunks)
-    hipError_t e = hipStreamSynchronize(h.l->stream);
+    hipError_t e = lane_sync(h.l->stream);
     if (rc == MEC_OK && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
     if (rc == MEC_OK) c->zc_calls++;
     return rc;

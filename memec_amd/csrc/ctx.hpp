@@ -218,6 +218,12 @@ bool is_multi(const mec_ctx *c);
 mec_ctx *shard_pick(mec_ctx *c);
 int shard_run(mec_ctx *c, uint32_t n, const std::function<int(mec_ctx *, uint32_t, uint32_t)> &fn);
 
+// Wait for a lane's single-call work.  Default: hipStreamSynchronize.
+// MEC_SYNC_SPIN=1 polls hipStreamQuery for up to 200 us first: +8 % calls/s
+// for one staged caller, but -14 % at 16 workers x RS(8,2)@4K (the pollers
+// compete for the cores the callers need) -- profiles/r01/host/sync_ab.log.
+hipError_t lane_sync(hipStream_t s);
+
 // batch.cpp
 void batch_release(mec_ctx *c);  // frees table slots and the host pipeline
 bool coalescing(mec_ctx *c);

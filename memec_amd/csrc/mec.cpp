@@ -4,7 +4,9 @@
 // coalescer live in batch.cpp.
 #include "ctx.hpp"
 
+#include <chrono>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 
@@ -163,6 +165,21 @@ Lane *lane_acquire(mec_ctx *c, int &rc) {
     return l;
 }
 
+hipError_t lane_sync(hipStream_t s) {
+    static const bool spin = [] {
+        const char *e = std::getenv("MEC_SYNC_SPIN");
+        return e && e[0] && e[0] != '0';
+    }();
+    if (spin) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200)) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e != hipErrorNotReady) return e;
+        }
+    }
+    return hipStreamSynchronize(s);
+}
+
 void lane_release(mec_ctx *c, Lane *l) {
     std::lock_guard<std::mutex> g(c->lane_mu);
     c->lanes_free.push_back(l);
@@ -199,7 +216,7 @@ int zc_single(mec_ctx *c, const std::vector<const uint8_t *> &srcs, const std::v
     uint8_t *b = reinterpret_cast<uint8_t *>(uintptr_t(base));
     rc = apply(c, b, 0, so, b, 0, dof, coef, 1, accumulate, h.l->stream);
     if (rc != MEC_OK) return rc;
-    HIP_TRY(hipStreamSynchronize(h.l->stream));
+    HIP_TRY(lane_sync(h.l->stream));
     c->zc_calls++;
     return MEC_OK;
 }
@@ -435,7 +452,7 @@ int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *pari
     for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(c->k + rows[r]) * int64_t(cs);
     rc = apply(c, h.l->hdev, 0, so, h.l->hdev, 0, dof, encode_rows(c, rows, cols), 1, false, h.l->stream);
     if (rc != MEC_OK) return rc;
-    HIP_TRY(hipStreamSynchronize(h.l->stream));
+    HIP_TRY(lane_sync(h.l->stream));
     for (size_t r = 0; r < rows.size(); ++r) std::memcpy(parity[rows[r]], h.l->host + dof[r], cs);
     return MEC_OK;
 }
@@ -473,7 +490,7 @@ int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
     for (size_t r = 0; r < dof.size(); ++r) dof[r] = int64_t(plan->dst[r]) * int64_t(cs);
     rc = apply(c, h.l->hdev, 0, so, h.l->hdev, 0, dof, plan->coef, 1, false, h.l->stream);
     if (rc != MEC_OK) return rc;
-    HIP_TRY(hipStreamSynchronize(h.l->stream));
+    HIP_TRY(lane_sync(h.l->stream));
     for (size_t r = 0; r < dof.size(); ++r) std::memcpy(chunks[plan->dst[r]], h.l->host + dof[r], cs);
     return MEC_OK;
 }
@@ -509,7 +526,7 @@ int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta
     }
     rc = apply(c, h.l->hdev, 0, so, h.l->hdev, 0, dof, encode_rows(c, rows, cols), 1, true, h.l->stream);
     if (rc != MEC_OK) return rc;
-    HIP_TRY(hipStreamSynchronize(h.l->stream));
+    HIP_TRY(lane_sync(h.l->stream));
     for (size_t r = 0; r < rows.size(); ++r) std::memcpy(parity[rows[r]], h.l->host + dof[r], cs);
     return MEC_OK;
 }
