@@ -109,7 +109,7 @@ typedef struct {
     uint64_t coalesced_requests; /* single-stripe requests they carried */
     uint64_t cached_plans;       /* decode plans cached (one per erasure pattern) */
     uint64_t zero_copy_calls;    /* host calls coded in place over PCIe (registered memory) */
-    uint64_t staged_calls;       /* host calls staged through HBM */
+    uint64_t staged_calls;       /* host calls copied through pinned, GPU-mapped staging */
 } mec_stats;
 
 typedef struct {
@@ -226,7 +226,7 @@ int mec_encode_host_batch(mec_ctx *ctx, const uint8_t *data, uint8_t *parity,
  * directly on the host chunks over PCIe: no staging copy, one launch per
  * call.  A server registers its ChunkPool slab once (chunk_pool.cc:22-47,
  * the 8-byte chunk headers included); chunks outside registered ranges are
- * staged through HBM as before.  mec_host_unregister takes the same ptr. */
+ * copied into pinned, GPU-mapped staging and coded there.  mec_host_unregister takes the same ptr. */
 int mec_host_register(void *ptr, size_t len);
 int mec_host_unregister(void *ptr);
 
@@ -238,7 +238,7 @@ int mec_host_unregister(void *ptr);
  * (the pointer arrays themselves are host arrays, consumed before return).
  * MEC_MEM_HOST: host pointers; synchronous, `stream` ignored.  Zero-copy
  * when every chunk lies in a mec_host_register range, otherwise staged
- * through HBM.
+ * through pinned, GPU-mapped host buffers.
  * Stripes are grouped by their linear map (same sources / outputs); each
  * group is one gather launch. */
 

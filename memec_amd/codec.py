@@ -141,8 +141,8 @@ class Codec:
     # ---- pointer-array batches (any memory kind) ----------------------------------
     # Pointers are integers (0 = NULL), one row per stripe: k data / m parity
     # for encode, k + m chunks for decode.  mem: "device" (CUDA tensor
-    # addresses, enqueued on the stream) or "host" (numpy addresses; staged
-    # through HBM, synchronous).
+    # addresses, enqueued on the stream) or "host" (numpy addresses,
+    # synchronous; zero-copy on registered memory, else pinned staging).
     @staticmethod
     def _ptr_array(ptrs):
         """uint64 numpy array (zero-copy) or a sequence of ints -> (void**, keepalive)."""

@@ -5,7 +5,7 @@
 // mec_host_register is mapped into the GPU's address space, so the coding
 // kernels read the k source chunks over PCIe and write the outputs straight
 // back — no staging copy through HBM and one launch per call.  Measured on
-// MI355X (tools/zerocopy_probe.hip, profiles/r01/zerocopy.log): the RS(10,4)
+// MI355X (tools/zerocopy_probe.hip, profiles/r01/host/zerocopy_probe.log): the RS(10,4)
 // stream reads host memory at 54.7 GB/s of data (PCIe Gen5 x16 both ways)
 // against 40.4 GB/s for H2D + kernel + D2H, and a single RS(8,2) 4 KiB
 // stripe takes 13.5 us instead of 20.6 us.
@@ -13,7 +13,10 @@
 // The registry maps registered host ranges to their device addresses; the
 // host entry points (mec_*_host, mec_*_batch with MEC_MEM_HOST,
 // mec_encode_host_batch) take the zero-copy path when every chunk of the
-// call lies in a registered range, and stage through HBM otherwise.
+// call lies in a registered range; otherwise they copy the chunks into
+// pinned, GPU-mapped staging and code there (still no HBM round trip).
+// Registration is Portable: on ROCm the locked range has one device address
+// valid on every GPU, so a multi-device context shares this registry.
 #include <map>
 #include <shared_mutex>
 
