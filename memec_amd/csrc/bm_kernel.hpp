@@ -76,14 +76,14 @@ __device__ __forceinline__ void bm_combine(const vec (&d)[W], vec (&acc)[ROWS], 
     }
 }
 
-template <int W, int R, bool G>
-__global__ __launch_bounds__(kThreads) void bm_kernel(const BmParams<W, R> p) {
+template <int W, int R, bool G, int BT>
+__global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
     constexpr int VW = bm_vw<W>();
     constexpr int ROWS = R * W;
     typedef typename VecT<VW>::type vec;
     const uint32_t bid = block_order(p.win);
     const uint32_t stripe = bid / p.tiles;
-    const uint32_t u = (bid - stripe * p.tiles) * kThreads + threadIdx.x;
+    const uint32_t u = (bid - stripe * p.tiles) * BT + threadIdx.x;
     if (u >= p.units) return;
     vec acc[ROWS];
     vec d[W], nx[W];
@@ -167,7 +167,10 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     p.dstride = L.dstride;
     p.chunk = uint32_t(L.packet * uint64_t(L.w));
     p.s0 = 0;
-    const Geometry g = geometry(L.packet / UB);
+    // block size from the whole launch's layout (sub-launches share it)
+    const uint32_t bt = block_threads(!L.stab, L.stab ? 1u : launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride,
+                                                                          L.dst, int64_t(L.n_stripes) * L.dst_stripe_stride));
+    const Geometry g = geometry(L.packet / UB, bt);
     p.units = g.units;
     p.tiles = g.tiles;
     p.accumulate = L.accumulate ? 1u : 0u;
@@ -182,12 +185,15 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
             if (L.stab) {
                 p.s0 = s0;
-                hipLaunchKernelGGL((bm_kernel<W, R, true>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                hipLaunchKernelGGL((bm_kernel<W, R, true, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
             } else {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
-                hipLaunchKernelGGL((bm_kernel<W, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                if (bt == kWaveBlock)
+                    hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
+                else
+                    hipLaunchKernelGGL((bm_kernel<W, R, false, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
             }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;

@@ -136,10 +136,10 @@ inline int gf8_structure(const Gf8Coef (*coef)[kMaxSrc], int k, int rows) {
 // caller's Chunk* arrays) instead of base + stripe * stride + offset; the
 // map stays in kernel arguments, so a block's only extra latency is one
 // batch of scalar loads of its pointers.
-template <int K, int R, bool G, int S>
-__global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) {
+template <int K, int R, bool G, int S, int BT>
+__global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     __shared__ uint32_t tab[R * K * 8];
-    for (int t = threadIdx.x; t < R * K; t += kThreads) {
+    for (int t = threadIdx.x; t < R * K; t += BT) {
         const Gf8Coef c = p.coef[t / K][t % K];
         tab[t * 8 + 0] = c.t0;
         tab[t * 8 + 1] = c.t1;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(kThreads) void gf8_kernel(const Gf8Params<K, R> p) 
     __syncthreads();
     const uint32_t bid = block_order(p.win);
     const uint32_t stripe = bid / p.tiles;
-    const uint32_t u = (bid - stripe * p.tiles) * kThreads + threadIdx.x;
+    const uint32_t u = (bid - stripe * p.tiles) * BT + threadIdx.x;
     if (u >= p.units) return;
     u32x4 d[K];
     u32x4 acc[R];
@@ -217,7 +217,10 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     p.dstride = L.dstride;
     p.chunk = uint32_t(L.len);
     p.s0 = 0;
-    const Geometry g = geometry(L.len / 16);
+    // block size from the whole launch's layout (sub-launches share it)
+    const uint32_t bt = block_threads(!L.stab, L.stab ? 1u : launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride,
+                                                                          L.dst, int64_t(L.n_stripes) * L.dst_stripe_stride));
+    const Geometry g = geometry(L.len / 16, bt);
     p.units = g.units;
     p.tiles = g.tiles;
     p.accumulate = L.accumulate ? 1u : 0u;
@@ -233,17 +236,25 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
             if (L.stab) {
                 p.s0 = s0;
                 if (vand)
-                    hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Vand>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                    hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Vand, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
                 else
-                    hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Dense>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                    hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Dense, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
             } else {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
-                if (vand)
-                    hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-                else
-                    hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Dense>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                const dim3 grid(ns * g.tiles), block(bt);
+                if (bt == kWaveBlock) {
+                    if (vand)
+                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand, kWaveBlock>), grid, block, 0, stream, p);
+                    else
+                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Dense, kWaveBlock>), grid, block, 0, stream, p);
+                } else {
+                    if (vand)
+                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand, kThreads>), grid, block, 0, stream, p);
+                    else
+                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Dense, kThreads>), grid, block, 0, stream, p);
+                }
             }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;

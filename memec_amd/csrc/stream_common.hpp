@@ -105,15 +105,27 @@ struct Geometry {
     uint32_t units, tiles, max_stripes_per_launch;
 };
 
-inline Geometry geometry(uint64_t full_units) {
+inline Geometry geometry(uint64_t full_units, uint32_t threads = kThreads) {
     Geometry g;
     g.units = uint32_t(full_units);
-    g.tiles = uint32_t((full_units + kThreads - 1) / kThreads);
+    g.tiles = uint32_t((full_units + threads - 1) / threads);
     if (g.tiles == 0) g.tiles = 1;
-    g.max_stripes_per_launch = uint32_t(((1ull << 31) / kThreads) / g.tiles);
+    g.max_stripes_per_launch = uint32_t(((1ull << 31) / threads) / g.tiles);
     if (g.max_stripes_per_launch == 0) g.max_stripes_per_launch = 1;
     return g;
 }
+
+// Threads per block of the gf8 / bitmatrix kernels.  One-wave blocks when
+// outputs are written away from the inputs (split data / parity, delta
+// updates): consecutive 1 KiB column slices then go to different XCDs, and
+// RS(10,4)@1 MiB encode gains 1 %, RS(10,4) update 2.3 %, RS(8,2)@4 KiB
+// 2 %.  In-place layouts (win > 1) keep 4-wave blocks: one-wave blocks lose
+// 1.4 % (RS) to 5 % (CRS) on in-place decode
+// (profiles/r01/layout/block_ab*.log).  Returns kWaveBlock or kThreads (a
+// kernel template argument, so the 256-thread code is unchanged);
+// MEC_BLOCK=64|256 overrides it per launch (experiments).
+constexpr int kWaveBlock = 64;
+uint32_t block_threads(bool strided, uint32_t win);
 
 }  // namespace detail
 }  // namespace mec

@@ -1,0 +1,11 @@
+#!/usr/bin/env bash
+# Round-final profiler evidence: the exact default bench command under
+# rocprofv3 --kernel-trace --stats (its bench line and kernel averages must
+# agree), then tools/gpu_session.sh prof for every bench config.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_default -o run \
+    -- python3 bench.py > gpurun_out/default_cmd_under_rocprof.json 2> gpurun_out/default_cmd_under_rocprof.err || exit $?
+PROF_CONFIGS="${PROF_CONFIGS:-rs_enc rs_dec crs_enc crs_dec rs8_small rs_update rs8_update}" bash tools/gpu_session.sh prof
