@@ -77,7 +77,7 @@
 extern "C" {
 #endif
 
-#define MEC_ABI_VERSION 2
+#define MEC_ABI_VERSION 3
 #define MEC_MAX_CHUNKS 32 /* k + m <= 32: RS_N_MAX / CRS_N_MAX (rscoding.hh:5, cauchycoding.hh:5) */
 
 typedef enum {
@@ -110,6 +110,8 @@ typedef struct {
     uint64_t cached_plans;       /* decode plans cached (one per erasure pattern) */
     uint64_t zero_copy_calls;    /* host calls coded in place over PCIe (registered memory) */
     uint64_t staged_calls;       /* host calls copied through pinned, GPU-mapped staging */
+    uint64_t queue_calls;        /* zero-copy calls served by the resident queue kernel */
+    uint64_t queue_launches;     /* launches of the resident queue kernel (idle exits relaunch) */
 } mec_stats;
 
 typedef struct {
@@ -273,6 +275,20 @@ int mec_encode_update_batch(mec_ctx *ctx, const uint32_t *data_index, const uint
  * of them as one host batch.  An idle context adds no wait.  0 = off
  * (default): every call is its own launch. */
 int mec_set_coalescing(mec_ctx *ctx, uint32_t max_batch);
+
+/* Device-side submission queue for single-stripe host calls (queue.hip).
+ * slots > 0 starts a resident kernel with one workgroup per slot, polling
+ * GPU-mapped host memory; mec_encode_host / mec_decode_host /
+ * mec_encode_update_host calls whose chunks are all registered
+ * (mec_host_register), of a byte-wise family (RS, ISA-L) and at most
+ * MEC_QUEUE_MAX_CHUNK bytes (default 16 KiB) are then posted to a free slot
+ * instead of launching a kernel: no HIP runtime call on the caller's path
+ * (calls beyond `slots` concurrent callers take the launch path).  The
+ * kernel exits after MEC_QUEUE_IDLE_MS (default 50) without work and is
+ * relaunched by the next call.  0 stops it.  Not to be called concurrently
+ * with other calls on the context.  Replaces nothing in the reference: its
+ * workers call the CPU plugin directly (worker.cc:128-137). */
+int mec_set_host_queue(mec_ctx *ctx, uint32_t slots);
 int mec_get_stats(const mec_ctx *ctx, mec_stats *out);
 
 #ifdef __cplusplus

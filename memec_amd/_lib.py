@@ -19,7 +19,7 @@ SYMBOLS = (
     "mec_get_matrix", "mec_get_bitmatrix", "mec_encode", "mec_decode", "mec_decode_split",
     "mec_encode_update", "mec_xor", "mec_fill_random", "mec_encode_host", "mec_decode_host",
     "mec_encode_update_host", "mec_encode_host_batch", "mec_host_register", "mec_host_unregister",
-    "mec_encode_batch", "mec_decode_batch", "mec_encode_update_batch", "mec_set_coalescing", "mec_get_stats",
+    "mec_encode_batch", "mec_decode_batch", "mec_encode_update_batch", "mec_set_coalescing", "mec_set_host_queue", "mec_get_stats",
 )
 MEM_DEVICE, MEM_HOST = 0, 1
 
@@ -39,7 +39,8 @@ class MecInfo(ctypes.Structure):
 class MecStats(ctypes.Structure):
     _fields_ = [("coalesced_batches", ctypes.c_uint64), ("coalesced_requests", ctypes.c_uint64),
                 ("cached_plans", ctypes.c_uint64), ("zero_copy_calls", ctypes.c_uint64),
-                ("staged_calls", ctypes.c_uint64)]
+                ("staged_calls", ctypes.c_uint64), ("queue_calls", ctypes.c_uint64),
+                ("queue_launches", ctypes.c_uint64)]
 
 
 _lib = None
@@ -85,6 +86,7 @@ def lib():
                                    ctypes.c_int, vp]
     L.mec_encode_update_batch.argtypes = [vp, ctypes.POINTER(u32), pvp, pvp, u32, u32, ctypes.c_int, vp]
     L.mec_set_coalescing.argtypes = [vp, u32]
+    L.mec_set_host_queue.argtypes = [vp, u32]
     L.mec_get_stats.argtypes = [vp, ctypes.POINTER(MecStats)]
     _lib = L
     return L

@@ -193,12 +193,18 @@ class Codec:
     def set_coalescing(self, max_batch):
         check(lib().mec_set_coalescing(self._h, max_batch))
 
+    def set_host_queue(self, slots):
+        """Resident submission-queue kernel for single-stripe calls on
+        registered host memory (mec_set_host_queue); 0 stops it."""
+        check(lib().mec_set_host_queue(self._h, slots))
+
     def stats(self):
         st = _lib.MecStats()
         check(lib().mec_get_stats(self._h, ctypes.byref(st)))
         return {"coalesced_batches": st.coalesced_batches, "coalesced_requests": st.coalesced_requests,
                 "cached_plans": st.cached_plans, "zero_copy_calls": st.zero_copy_calls,
-                "staged_calls": st.staged_calls}
+                "staged_calls": st.staged_calls, "queue_calls": st.queue_calls,
+                "queue_launches": st.queue_launches}
 
 
 def fill_random(t, seed, word_offset=0, stream=None):

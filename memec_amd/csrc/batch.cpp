@@ -899,6 +899,8 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
     out->coalesced_requests = c->coal.requests;
     out->zero_copy_calls = c->zc_calls.load();
     out->staged_calls = c->staged_calls.load();
+    out->queue_calls = c->hq ? c->hq->calls.load() : 0;
+    out->queue_launches = c->hq ? c->hq->launches.load() : 0;
     {
         std::lock_guard<std::mutex> pk(c->plan_mu);
         out->cached_plans = c->plans.size();
@@ -911,6 +913,8 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
         out->cached_plans += t.cached_plans;
         out->zero_copy_calls += t.zero_copy_calls;
         out->staged_calls += t.staged_calls;
+        out->queue_calls += t.queue_calls;
+        out->queue_launches += t.queue_launches;
     }
     return MEC_OK;
 }

@@ -37,6 +37,16 @@ static unsigned adapter_coalesce() {
     return e ? unsigned(atoi(e)) : 0u;
 }
 
+// Resident submission-queue kernel for single-stripe calls on registered
+// chunks (mec_set_host_queue), on by default with 32 slots: with 16 workers
+// it serves 2.9x (RS(8,2)@4 KiB seal) to 3.4x (RS(10,4)@4 KiB delta) the
+// calls/s of per-call launches (profiles/r01/host/queue_ab.log).
+// MEMEC_GPU_QUEUE = slots, 0 = off.
+static unsigned adapter_queue() {
+    const char *e = getenv("MEMEC_GPU_QUEUE");
+    return e ? unsigned(atoi(e)) : 32u;
+}
+
 GpuMatrixCoding::GpuMatrixCoding(int family, const char *name, uint32_t k, uint32_t m, uint32_t chunkSize)
     : _name(name), _family(family), _k(k), _m(m), _chunkSize(chunkSize), _ctx(0) {
     // Parameter errors exit(-1) with a message, like rscoding.cc:26-29 and
@@ -51,6 +61,8 @@ GpuMatrixCoding::GpuMatrixCoding(int family, const char *name, uint32_t k, uint3
     }
     if (adapter_coalesce() && mec_set_coalescing(_ctx, adapter_coalesce()) != MEC_OK)
         fprintf(stderr, "%s: coalescing unavailable: %s\n", _name, mec_last_error());
+    if (adapter_queue() && mec_set_host_queue(_ctx, adapter_queue()) != MEC_OK)
+        fprintf(stderr, "%s: host queue unavailable: %s\n", _name, mec_last_error());
 }
 
 GpuMatrixCoding::~GpuMatrixCoding() { mec_destroy(_ctx); }

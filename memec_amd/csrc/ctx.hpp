@@ -105,6 +105,29 @@ struct Coalescer {
     uint64_t batches = 0, requests = 0;  // statistics
 };
 
+// queue.hip: device-side submission queue for single-stripe host calls.
+constexpr uint32_t kQMaxSrc = 32, kQMaxDst = 4, kQMaxSlots = 1024;
+struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
+    uint64_t seq;            // host -> GPU: number of the posted job
+    uint64_t pad0[15];
+    uint64_t done;           // GPU -> host: number of the last finished job
+    uint64_t pad1[15];
+    uint32_t hdr[4];         // sources, outputs, chunk bytes, accumulate
+    uint64_t src[kQMaxSrc];  // device addresses of registered chunks (0 = zeros)
+    uint64_t dst[kQMaxDst];  // (0 = unwanted output)
+    uint32_t coef_w[kQMaxDst * kQMaxSrc / 4];  // GF(2^8) bytes, [output][source]
+};
+struct HostQueue {
+    QSlot *host = nullptr, *dev = nullptr;
+    uint32_t *stop_host = nullptr, *stop_dev = nullptr;
+    uint32_t slots = 0, max_chunk = 0, threads = 0;
+    uint64_t idle_ticks = 0;
+    std::atomic<bool> *busy = nullptr;
+    hipStream_t stream = nullptr;
+    std::mutex mu;  // launches
+    std::atomic<uint64_t> calls{0}, launches{0};
+};
+
 }  // namespace core
 }  // namespace mec
 
@@ -130,6 +153,8 @@ struct mec_ctx {
     mec::core::HostPipe pipe;
     mec::core::Coalescer coal;
     std::atomic<uint64_t> zc_calls{0}, staged_calls{0};  // host-call statistics
+    std::mutex hq_mu;
+    mec::core::HostQueue *hq = nullptr;  // mec_set_host_queue
     // multi-GPU context (multi.cpp): one ordinary context per device
     std::vector<mec_ctx *> shards;
     std::atomic<uint32_t> rr{0};
@@ -223,6 +248,12 @@ int shard_run(mec_ctx *c, uint32_t n, const std::function<int(mec_ctx *, uint32_
 // for one staged caller, but -14 % at 16 workers x RS(8,2)@4K (the pollers
 // compete for the cores the callers need) -- profiles/r01/host/sync_ab.log.
 hipError_t lane_sync(hipStream_t s);
+
+// queue.hip.  queue_try: run one zero-copy call (addrs = ns sources then nd
+// outputs, device addresses) through the resident kernel; false = not
+// eligible or no free slot (nothing done), else rc holds the result.
+bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Mat &coef, bool accumulate, int &rc);
+void queue_stop(mec_ctx *c);
 
 // batch.cpp
 void batch_release(mec_ctx *c);  // frees table slots and the host pipeline

@@ -205,6 +205,13 @@ int zc_single(mec_ctx *c, const std::vector<const uint8_t *> &srcs, const std::v
             for (uint8_t *o : outs) std::memset(o, 0, cs);
         return MEC_OK;
     }
+    {
+        int qrc = MEC_OK;
+        if (c->hq && queue_try(c, a.data(), srcs.size(), outs.size(), coef, accumulate, qrc)) {
+            if (qrc == MEC_OK) c->zc_calls++;
+            return qrc;
+        }
+    }
     DeviceGuard dg(c->device);
     int rc = MEC_OK;
     LaneHold h{c, lane_acquire(c, rc)};
@@ -297,6 +304,7 @@ void mec_destroy(mec_ctx *c) {
     c->shards.clear();
     if (has_device(c)) {
         DeviceGuard g(c->device);
+        queue_stop(c);  // the resident kernel returns before anything is freed
         batch_release(c);
         for (Lane *l : c->lanes_all) {
             (void)hipStreamSynchronize(l->stream);

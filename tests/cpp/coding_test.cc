@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "coding.hh"
+#include "mec.h"
 
 static int fails = 0;
 #define EXPECT(cond, ...)                                   \
@@ -32,11 +33,29 @@ struct Stripe {
     uint32_t k, m, cs;
     TempChunkPool pool;
     std::vector<Chunk *> c;
+    bool reg;  // CODING_TEST_REGISTER=1: chunks registered (zero-copy / host queue)
     Stripe(uint32_t k_, uint32_t m_, uint32_t cs_) : k(k_), m(m_), cs(cs_), c(k_ + m_) {
-        for (auto &x : c) x = pool.alloc();
+        reg = getenv("CODING_TEST_REGISTER") && atoi(getenv("CODING_TEST_REGISTER"));
+        for (auto &x : c) {
+            if (!reg) {
+                x = pool.alloc();
+                continue;
+            }
+            // whole pages per chunk, so no two registrations share a page
+            const size_t bytes = (ChunkUtil::chunkSize + 8 + 4095) / 4096 * 4096;
+            x = (Chunk *)aligned_alloc(4096, bytes);
+            ChunkUtil::clear(x);
+            if (mec_host_register(x, bytes) != MEC_OK) {
+                fprintf(stderr, "mec_host_register: %s\n", mec_last_error());
+                exit(1);
+            }
+        }
     }
     ~Stripe() {
-        for (auto &x : c) pool.free(x);
+        for (auto &x : c) {
+            if (reg) mec_host_unregister(x);
+            pool.free(x);  // free() either way
+        }
     }
     char *data(uint32_t i) { return ChunkUtil::getData(c[i]); }
 };

@@ -48,13 +48,16 @@ def test_coding_flow_on_gpu(binaries, args):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"MEMEC_GPU_DEVICES": "0,0"}, {"MEMEC_GPU_COALESCE": "64"}])
+@pytest.mark.parametrize("env", [{"MEMEC_GPU_DEVICES": "0,0"}, {"MEMEC_GPU_COALESCE": "64"},
+                                 {"CODING_TEST_REGISTER": "1"}, {"CODING_TEST_REGISTER": "1", "MEMEC_GPU_QUEUE": "0"}])
 def test_coding_flow_adapter_modes(binaries, env):
     """The same flow with the adapter driving a multi-device context
-    (MEMEC_GPU_DEVICES, device repeated on a one-GPU box) and with the
-    request coalescer on."""
+    (MEMEC_GPU_DEVICES, device repeated on a one-GPU box), with the request
+    coalescer on, and on registered chunks (zero-copy; single-stripe calls
+    through the resident host queue unless MEMEC_GPU_QUEUE=0)."""
     for b in binaries:
-        for args in (["rs", "10", "4", "65536"], ["cauchy", "12", "4", "65536"]):
+        for args in (["rs", "10", "4", "65536"], ["cauchy", "12", "4", "65536"], ["rs", "8", "3", "4096"],
+                     ["rs", "6", "2", "4104"]):
             r = subprocess.run([b] + args, capture_output=True, text=True, timeout=120,
                                env=dict(os.environ, **env))
             assert r.returncode == 0, (b, args, env, r.stdout, r.stderr)

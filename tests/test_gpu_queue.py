@@ -1,0 +1,221 @@
+"""GPU parity of the device-side submission queue (mec_set_host_queue,
+memec_amd/csrc/queue.hip): single-stripe host calls on registered chunks
+posted to a resident kernel instead of launched.  Bit-exact against the
+oracle for encode(index) / decode / delta update, under concurrent callers
+(MemEC's workers share one Coding, worker.cc:128-137), across an idle exit
+and relaunch, and with the launch path taking what the queue does not serve
+(bitmatrix Cauchy, chunks above MEC_QUEUE_MAX_CHUNK, unregistered chunks,
+queue stopped).
+"""
+import ctypes
+import os
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import _oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from memec_amd import Codec, host_register, host_unregister  # noqa: E402
+from memec_amd._lib import check, lib  # noqa: E402
+
+vp = ctypes.c_void_p
+BYTEWISE = ["rs", "isal_rs", "isal_cauchy"]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    yield
+    torch.cuda.synchronize()
+
+
+def aligned(nbytes, align=4096):
+    raw = np.empty(nbytes + align, np.uint8)
+    off = (-raw.ctypes.data) % align
+    return raw[off:off + nbytes]
+
+
+class Slab:
+    """Registered ChunkPool-like slab: slots of 8 + cs bytes (chunk_pool.cc:22-95)."""
+
+    def __init__(self, n, cs, seed):
+        self.cs, self.slot = cs, cs + 8
+        self.buf = aligned(n * self.slot)
+        self.buf[:] = O.fill(self.buf.nbytes, seed)
+        host_register(self.buf)
+
+    def close(self):
+        host_unregister(self.buf)
+
+    def addr(self, i):
+        return self.buf.ctypes.data + i * self.slot + 8
+
+    def view(self, i):
+        o = i * self.slot + 8
+        return self.buf[o:o + self.cs]
+
+
+def encode_index(c, slab, k, dslots, pslot, index):
+    """Coding::encode(data, parity, index): parity row index-1 only."""
+    dp = (vp * k)(*[vp(slab.addr(s)) if s is not None else vp() for s in dslots])
+    pp = (vp * c.m)(*[vp(slab.addr(pslot)) if i == index - 1 else vp() for i in range(c.m)])
+    check(lib().mec_encode_host(c._h, dp, pp))
+
+
+@pytest.mark.parametrize("fam", BYTEWISE)
+@pytest.mark.parametrize("k,m,cs", [(8, 2, 4096), (10, 4, 16384), (4, 2, 4104), (12, 4, 1024), (20, 4, 2048)])
+def test_queue_encode_decode_update(fam, k, m, cs):
+    slab = Slab(k + m + 1, cs, 31 + k)
+    c = Codec(fam, k, m, cs)
+    try:
+        c.set_host_queue(8)
+        data = [slab.view(j).copy() for j in range(k)]
+        want = O.encode(fam, k, m, [d.copy() for d in data], cs)
+        q0 = c.stats()["queue_calls"]
+        for i in range(m):  # the SEAL pattern: encode(index) for every parity
+            encode_index(c, slab, k, list(range(k)), k + i, i + 1)
+        for i in range(m):
+            assert np.array_equal(slab.view(k + i), want[i]), (fam, i)
+        assert c.stats()["queue_calls"] == q0 + m
+        # Coding::zeros sources (NULL) in a single-column encode
+        single = [None] * k
+        single[2] = 2
+        encode_index(c, slab, k, single, k + m, 1)
+        z = [np.zeros(cs, np.uint8)] * k
+        z = list(z)
+        z[2] = data[2].copy()
+        assert np.array_equal(slab.view(k + m), O.encode(fam, k, m, z, cs)[0])
+        # decode in place, data and parity erased
+        orig = [slab.view(i).copy() for i in range(k + m)]
+        pat = sorted({0, k - 1, k, k + m - 1})[:m]
+        for e in pat:
+            slab.view(e)[:] = 0
+        c.decode_host([slab.view(i) for i in range(k + m)], sum(1 << i for i in range(k + m) if i not in pat))
+        for i in range(k + m):
+            assert np.array_equal(slab.view(i), orig[i]), (fam, pat, i)
+        # delta update of every parity (the spare slot holds the delta)
+        delta = slab.view(k + m)
+        d2 = [o.copy() for o in orig[:k]]
+        d2[1] ^= delta
+        c.encode_update_host(1, delta, [slab.view(k + i) for i in range(m)])
+        want2 = O.encode(fam, k, m, d2, cs)
+        for i in range(m):
+            assert np.array_equal(slab.view(k + i), want2[i]), (fam, i)
+        st = c.stats()
+        assert st["queue_calls"] == q0 + m + 3 and st["queue_launches"] >= 1
+    finally:
+        c.close()
+        slab.close()
+
+
+def test_queue_concurrent_callers():
+    """16 threads share one context; every call's parity checked."""
+    k, m, cs, T, per = 8, 2, 4096, 16, 40
+    slab = Slab(T * (k + m), cs, 5)
+    c = Codec("rs", k, m, cs)
+    errs = []
+    try:
+        c.set_host_queue(8)  # fewer slots than callers: the rest take the launch path
+        wants = [O.encode("rs", k, m, [slab.view(t * (k + m) + j).copy() for j in range(k)], cs) for t in range(T)]
+        st0 = c.stats()
+
+        def worker(t):
+            try:
+                base = t * (k + m)
+                for n in range(per):
+                    i = n % m
+                    slab.view(base + k + i)[:] = 0
+                    encode_index(c, slab, k, [base + j for j in range(k)], base + k + i, i + 1)
+                    if not np.array_equal(slab.view(base + k + i), wants[t][i]):
+                        errs.append((t, n))
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errs, errs[:5]
+        st = c.stats()
+        served = st["queue_calls"] - st0["queue_calls"]
+        launched = st["zero_copy_calls"] - st0["zero_copy_calls"] - served
+        assert served > 0 and served + launched == T * per
+    finally:
+        c.close()
+        slab.close()
+
+
+def test_queue_idle_exit_and_relaunch():
+    k, m, cs = 6, 3, 8192
+    os.environ["MEC_QUEUE_IDLE_MS"] = "5"
+    slab = Slab(k + m, cs, 8)
+    c = Codec("rs", k, m, cs)
+    try:
+        c.set_host_queue(4)
+        want = O.encode("rs", k, m, [slab.view(j).copy() for j in range(k)], cs)
+        for rnd in range(4):
+            slab.view(k)[:] = 0
+            encode_index(c, slab, k, list(range(k)), k, 1)
+            assert np.array_equal(slab.view(k), want[0]), rnd
+            time.sleep(0.05)  # > idle: the resident kernel exits
+        st = c.stats()
+        assert st["queue_calls"] == 4 and st["queue_launches"] >= 2
+    finally:
+        os.environ.pop("MEC_QUEUE_IDLE_MS", None)
+        c.close()
+        slab.close()
+
+
+def test_queue_fallbacks():
+    """Calls the queue does not serve still code correctly through launches."""
+    k, m = 4, 2
+    # bitmatrix Cauchy: not byte-wise
+    slab = Slab(k + m, 4096, 3)
+    c = Codec("cauchy", k, m, 4096)
+    try:
+        c.set_host_queue(4)
+        want = O.encode("cauchy", k, m, [slab.view(j).copy() for j in range(k)], 4096)
+        encode_index(c, slab, k, list(range(k)), k, 1)
+        assert np.array_equal(slab.view(k), want[0])
+        st = c.stats()
+        assert st["queue_calls"] == 0 and st["zero_copy_calls"] == 1
+    finally:
+        c.close()
+        slab.close()
+    # chunk above MEC_QUEUE_MAX_CHUNK, then the queue stopped
+    cs = 128 << 10
+    slab = Slab(k + m, cs, 4)
+    c = Codec("rs", k, m, cs)
+    try:
+        c.set_host_queue(4)
+        want = O.encode("rs", k, m, [slab.view(j).copy() for j in range(k)], cs)
+        encode_index(c, slab, k, list(range(k)), k + 1, 2)
+        assert np.array_equal(slab.view(k + 1), want[1])
+        assert c.stats()["queue_calls"] == 0
+        c.set_host_queue(0)
+        slab.view(k + 1)[:] = 0
+        encode_index(c, slab, k, list(range(k)), k + 1, 2)
+        assert np.array_equal(slab.view(k + 1), want[1])
+    finally:
+        c.close()
+        slab.close()
+    # unregistered chunks: staged
+    c = Codec("rs", k, m, 4096)
+    try:
+        c.set_host_queue(4)
+        data = [O.fill(4096, 70 + j) for j in range(k)]
+        got = c.encode_host(data)
+        want = O.encode("rs", k, m, [d.copy() for d in data], 4096)
+        for i in range(m):
+            assert np.array_equal(got[i], want[i])
+        assert c.stats()["queue_calls"] == 0
+    finally:
+        c.close()
