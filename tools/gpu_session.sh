@@ -30,7 +30,7 @@ run() {  # name seconds cmd...
 
 for step in "$@"; do
     case $step in
-        tests) run pytest_gpu 1100 python -m pytest tests -m gpu -x -q ;;
+        tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py ;;
         benchall)
