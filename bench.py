@@ -17,6 +17,7 @@ average launch time from HIP events on the launch stream.
 import argparse
 import json
 import os
+import re
 import sys
 import time
 
@@ -51,6 +52,18 @@ WORKLOAD_NAMES = {
     "rs8_update": "RS(8,2) delta update of data column 3 into both parities, 4 KiB chunks, 65536 stripes per GPU",
     "rs_update": "RS(10,4) delta update of data column 3 into all 4 parities, 1 MiB chunks, 4096 stripes per GPU",
 }
+
+
+def workload_name(config, stripes, strong=False, global_stripes=0):
+    """WORKLOAD_NAMES[config] with the stripe count actually run (--stripes /
+    --strong override the BASELINE count; the name must not claim it then)."""
+    name = WORKLOAD_NAMES[config]
+    m = re.search(r"(\d+) stripes per GPU", name)
+    if strong:
+        return name[:m.start()] + "%d stripes total, sharded over ranks" % global_stripes + name[m.end():]
+    if int(m.group(1)) != stripes:
+        return name[:m.start()] + "%d stripes per GPU (reduced)" % stripes + name[m.end():]
+    return name
 
 
 def cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads):
@@ -306,7 +319,7 @@ def main():
         dwall, dkern = timed_steps(lambda: codec.decode(st, dpresent), args.steps, args.warmup,
                                    sync=torch.cuda.synchronize, dist=dist if world > 1 else None, events=dev_ev)
         dalg = (k + len(derased)) * cs * stripes
-        secondary = {"workload": WORKLOAD_NAMES[twin], "erased": derased,
+        secondary = {"workload": workload_name(twin, stripes, args.strong, global_stripes), "erased": derased,
                      "value": round(global_stripes * k * cs * args.steps / dwall / 2**30, 3), "unit": "GiB/s",
                      "ms_per_step": round(dwall / args.steps * 1e3, 4), "kernel_ms": round(dkern, 4),
                      "achieved_GBps": round(dalg / (dkern * 1e-3) / 1e9, 1),
@@ -404,7 +417,7 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (splitmix64 stripes generated in HBM)",
-            "config": {"workload": WORKLOAD_NAMES[args.config], "family": fam, "k": k, "m": m,
+            "config": {"workload": workload_name(args.config, stripes, args.strong, global_stripes), "family": fam, "k": k, "m": m,
                        "chunk_bytes": cs, "stripes_per_gpu": stripes, "global_stripes": global_stripes,
                        "op": op, "erased": erased, "parallelism": "stripe-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
