@@ -279,11 +279,12 @@ int mec_set_coalescing(mec_ctx *ctx, uint32_t max_batch);
 /* Device-side submission queue for single-stripe host calls (queue.hip).
  * slots > 0 starts a resident kernel with one workgroup per slot, polling
  * GPU-mapped host memory; mec_encode_host / mec_decode_host /
- * mec_encode_update_host calls whose chunks are all registered
- * (mec_host_register), of a byte-wise family (RS, ISA-L) and at most
- * MEC_QUEUE_MAX_CHUNK bytes (default 16 KiB) are then posted to a free slot
- * instead of launching a kernel: no HIP runtime call on the caller's path
- * (calls beyond `slots` concurrent callers take the launch path).  The
+ * mec_encode_update_host calls of a byte-wise family (RS, ISA-L) with
+ * chunks of at most MEC_QUEUE_MAX_CHUNK bytes (default 16 KiB) are then
+ * posted to a free slot instead of launching a kernel: no HIP runtime call
+ * on the caller's path (calls beyond `slots` concurrent callers take the
+ * launch path).  Registered chunks (mec_host_register) are coded in place;
+ * other host chunks are copied through a mapped pinned staging buffer.  The
  * kernel exits after MEC_QUEUE_IDLE_MS (default 50) without work and is
  * relaunched by the next call.  0 stops it.  Not to be called concurrently
  * with other calls on the context.  Replaces nothing in the reference: its

@@ -229,6 +229,33 @@ int zc_single(mec_ctx *c, const std::vector<const uint8_t *> &srcs, const std::v
 }
 
 
+// Run one staged single-stripe call whose chunks sit in lane l's mapped
+// pinned buffer (offsets so / dof): the resident queue kernel
+// (mec_set_host_queue) codes them in place when it can take the call,
+// otherwise one launch on the lane's stream and a wait.  A queue call that
+// never completes leaves its workgroup owning the buffer, so the lane is
+// then retired instead of returned to the pool.
+int lane_run(mec_ctx *c, LaneHold &h, const std::vector<int64_t> &so, const std::vector<int64_t> &dof,
+             const Mat &coef, bool accumulate) {
+    Lane *l = h.l;
+    if (c->hq) {
+        const uint64_t base = uint64_t(uintptr_t(l->hdev));
+        std::vector<uint64_t> a(so.size() + dof.size());
+        for (size_t t = 0; t < so.size(); ++t) a[t] = base + uint64_t(so[t]);
+        for (size_t r = 0; r < dof.size(); ++r) a[so.size() + r] = base + uint64_t(dof[r]);
+        int qrc = MEC_OK;
+        if (queue_try(c, a.data(), so.size(), dof.size(), coef, accumulate, qrc)) {
+            if (qrc != MEC_OK) h.l = nullptr;
+            return qrc;
+        }
+    }
+    int rc = apply(c, l->hdev, 0, so, l->hdev, 0, dof, coef, 1, accumulate, l->stream);
+    if (rc != MEC_OK) return rc;
+    HIP_TRY(lane_sync(l->stream));
+    return MEC_OK;
+}
+
+
 }  // namespace core
 }  // namespace mec
 
@@ -458,9 +485,8 @@ int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *pari
         std::memcpy(h.l->host + so[t], data[cols[t]], cs);
     }
     for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(c->k + rows[r]) * int64_t(cs);
-    rc = apply(c, h.l->hdev, 0, so, h.l->hdev, 0, dof, encode_rows(c, rows, cols), 1, false, h.l->stream);
+    rc = lane_run(c, h, so, dof, encode_rows(c, rows, cols), false);
     if (rc != MEC_OK) return rc;
-    HIP_TRY(lane_sync(h.l->stream));
     for (size_t r = 0; r < rows.size(); ++r) std::memcpy(parity[rows[r]], h.l->host + dof[r], cs);
     return MEC_OK;
 }
@@ -496,9 +522,8 @@ int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
         std::memcpy(h.l->host + so[t], chunks[plan->src[t]], cs);
     }
     for (size_t r = 0; r < dof.size(); ++r) dof[r] = int64_t(plan->dst[r]) * int64_t(cs);
-    rc = apply(c, h.l->hdev, 0, so, h.l->hdev, 0, dof, plan->coef, 1, false, h.l->stream);
+    rc = lane_run(c, h, so, dof, plan->coef, false);
     if (rc != MEC_OK) return rc;
-    HIP_TRY(lane_sync(h.l->stream));
     for (size_t r = 0; r < dof.size(); ++r) std::memcpy(chunks[plan->dst[r]], h.l->host + dof[r], cs);
     return MEC_OK;
 }
@@ -532,9 +557,8 @@ int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta
         dof[r] = int64_t(1 + r) * int64_t(cs);
         std::memcpy(h.l->host + dof[r], parity[rows[r]], cs);
     }
-    rc = apply(c, h.l->hdev, 0, so, h.l->hdev, 0, dof, encode_rows(c, rows, cols), 1, true, h.l->stream);
+    rc = lane_run(c, h, so, dof, encode_rows(c, rows, cols), true);
     if (rc != MEC_OK) return rc;
-    HIP_TRY(lane_sync(h.l->stream));
     for (size_t r = 0; r < rows.size(); ++r) std::memcpy(parity[rows[r]], h.l->host + dof[r], cs);
     return MEC_OK;
 }

@@ -23,9 +23,11 @@
 // Launches of the resident kernel go to one stream, so two instances never
 // run at once.
 //
-// Scope: byte-wise families (RS, ISA-L) on zero-copy (registered) chunks of
-// at most MEC_QUEUE_MAX_CHUNK bytes (default 16 KiB; larger chunks want the
-// whole GPU, so they keep the launch path).
+// Scope: byte-wise families (RS, ISA-L), chunks of at most
+// MEC_QUEUE_MAX_CHUNK bytes (default 16 KiB; larger chunks want the whole
+// GPU, so they keep the launch path), either zero-copy (registered) or
+// staged: unregistered chunks are copied into a lane's mapped pinned buffer
+// and the workgroup codes that buffer in place (mec.cpp lane_run).
 #include <hip/hip_runtime.h>
 
 #include <chrono>

@@ -4,8 +4,8 @@ posted to a resident kernel instead of launched.  Bit-exact against the
 oracle for encode(index) / decode / delta update, under concurrent callers
 (MemEC's workers share one Coding, worker.cc:128-137), across an idle exit
 and relaunch, and with the launch path taking what the queue does not serve
-(bitmatrix Cauchy, chunks above MEC_QUEUE_MAX_CHUNK, unregistered chunks,
-queue stopped).
+(bitmatrix Cauchy, chunks above MEC_QUEUE_MAX_CHUNK, queue stopped).
+Unregistered (staged) chunks reach the queue through mapped pinned lanes.
 """
 import ctypes
 import os
@@ -207,15 +207,88 @@ def test_queue_fallbacks():
     finally:
         c.close()
         slab.close()
-    # unregistered chunks: staged
-    c = Codec("rs", k, m, 4096)
+    # unregistered chunks above the queue's chunk limit: staged + launched
+    cs = 128 << 10
+    c = Codec("rs", k, m, cs)
     try:
         c.set_host_queue(4)
-        data = [O.fill(4096, 70 + j) for j in range(k)]
+        data = [O.fill(cs, 70 + j) for j in range(k)]
         got = c.encode_host(data)
-        want = O.encode("rs", k, m, [d.copy() for d in data], 4096)
+        want = O.encode("rs", k, m, [d.copy() for d in data], cs)
         for i in range(m):
             assert np.array_equal(got[i], want[i])
-        assert c.stats()["queue_calls"] == 0
+        st = c.stats()
+        assert st["queue_calls"] == 0 and st["staged_calls"] == 1
+    finally:
+        c.close()
+
+
+@pytest.mark.parametrize("fam", BYTEWISE)
+@pytest.mark.parametrize("k,m,cs", [(8, 2, 4096), (10, 4, 16384), (4, 2, 4104), (20, 4, 2048)])
+def test_queue_staged_calls(fam, k, m, cs):
+    """Unregistered host chunks go through a lane's mapped pinned buffer to
+    the resident kernel.  The same lanes are reused call after call with new
+    contents, so stale lines from an earlier call would show up here."""
+    c = Codec(fam, k, m, cs)
+    try:
+        c.set_host_queue(4)
+        st0 = c.stats()
+        for rnd in range(6):
+            data = [O.fill(cs, 1000 * rnd + 10 * k + j) for j in range(k)]
+            want = O.encode(fam, k, m, [d.copy() for d in data], cs)
+            got = c.encode_host(data)
+            for i in range(m):
+                assert np.array_equal(got[i], want[i]), (rnd, i)
+            chunks = [d.copy() for d in data] + [w.copy() for w in want]
+            pat = sorted({rnd % k, k - 1, k + rnd % m})[:m]
+            for e in pat:
+                chunks[e][:] = 0
+            c.decode_host(chunks, sum(1 << i for i in range(k + m) if i not in pat))
+            for i in range(k + m):
+                assert np.array_equal(chunks[i], data[i] if i < k else want[i - k]), (rnd, pat, i)
+            delta = O.fill(cs, 7777 + rnd)
+            par = [w.copy() for w in want]
+            c.encode_update_host(rnd % k, delta, par)
+            d2 = [d.copy() for d in data]
+            d2[rnd % k] ^= delta
+            want2 = O.encode(fam, k, m, d2, cs)
+            for i in range(m):
+                assert np.array_equal(par[i], want2[i]), (rnd, i)
+        st = c.stats()
+        assert st["queue_calls"] - st0["queue_calls"] == 18
+        assert st["staged_calls"] - st0["staged_calls"] == 18
+    finally:
+        c.close()
+
+
+def test_queue_staged_concurrent_callers():
+    """16 threads of unregistered single-stripe encodes through 8 slots."""
+    k, m, cs, T, per = 8, 2, 4096, 16, 30
+    c = Codec("rs", k, m, cs)
+    errs = []
+    try:
+        c.set_host_queue(8)
+        st0 = c.stats()
+
+        def worker(t):
+            try:
+                for n in range(per):
+                    data = [O.fill(cs, 100000 * t + 100 * n + j) for j in range(k)]
+                    want = O.encode("rs", k, m, [d.copy() for d in data], cs)
+                    got = c.encode_host(data)
+                    if not all(np.array_equal(got[i], want[i]) for i in range(m)):
+                        errs.append((t, n))
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errs, errs[:5]
+        st = c.stats()
+        assert st["staged_calls"] - st0["staged_calls"] == T * per
+        assert st["queue_calls"] - st0["queue_calls"] > 0
     finally:
         c.close()
