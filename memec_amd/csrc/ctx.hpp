@@ -121,6 +121,8 @@ struct HostQueue {
     QSlot *host = nullptr, *dev = nullptr;
     uint32_t *stop_host = nullptr, *stop_dev = nullptr;
     uint32_t slots = 0, max_chunk = 0, threads = 0;
+    uint32_t solo_max = 0;            // larger chunks use the queue only beside other queue calls
+    std::atomic<uint32_t> inflight{0};
     uint64_t idle_ticks = 0;
     std::atomic<bool> *busy = nullptr;
     hipStream_t stream = nullptr;

@@ -244,6 +244,9 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     std::unique_ptr<HostQueue> q(new HostQueue);
     q->slots = slots;
     q->max_chunk = uint32_t(env_u64("MEC_QUEUE_MAX_CHUNK", 16 << 10));
+    // a lone call on a chunk above this codes faster as a launch (many
+    // workgroups over PCIe) than on one queue workgroup
+    q->solo_max = uint32_t(env_u64("MEC_QUEUE_SOLO_MAX", q->max_chunk));
     q->idle_ticks = env_u64("MEC_QUEUE_IDLE_MS", 50) * 100000ull;  // s_memrealtime: 100 MHz
     // one 16-byte unit per thread up to kQThreads (a 4 KiB chunk: 256 threads;
     // idle threads only cost barrier time), at least 128 (descriptor loads)
@@ -288,6 +291,7 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     HostQueue *q = c->hq;
     if (!q || !c->byte_wise() || c->cs > q->max_chunk || ns > kQMaxSrc || nd > kQMaxDst || nd == 0)
         return false;
+    if (c->cs > q->solo_max && q->inflight.load(std::memory_order_relaxed) == 0) return false;
     // a free slot, starting from a per-thread hint so callers spread out
     static thread_local uint32_t hint = uint32_t(std::hash<std::thread::id>()(std::this_thread::get_id()));
     uint32_t i = 0;
@@ -299,6 +303,7 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     }
     if (!got) return false;  // every slot busy: the launch path takes this call
     hint = i;
+    q->inflight.fetch_add(1, std::memory_order_relaxed);
     QSlot *s = q->host + i;
     s->hdr[0] = uint32_t(ns);
     s->hdr[1] = uint32_t(nd);
@@ -329,6 +334,7 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
         }
         __builtin_ia32_pause();
     }
+    q->inflight.fetch_sub(1, std::memory_order_relaxed);
     if (rc == MEC_OK) {
         q->busy[i].store(false, std::memory_order_release);
         q->calls++;
