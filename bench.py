@@ -104,6 +104,95 @@ def cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads):
             "single_thread_value": round(single, 4), "matches_gpu": verified, "cpu_model": cpu_model()}
 
 
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libmemec_ref.so")
+
+
+def _ref_lib():
+    """The reference's own coding path (MemEC plugin + Jerasure +
+    gf_complete) compiled from its sources in the build container by
+    oracle/Makefile into oracle/_ref/ (travels with the tree; absent in a
+    fresh checkout -> None).  Used only for the CPU baseline."""
+    import ctypes
+    if not os.path.exists(REF_SO):
+        return None
+    L = ctypes.CDLL(REF_SO)
+    vp, u32 = ctypes.c_void_p, ctypes.c_uint32
+    L.ref_instantiate.restype = vp
+    L.ref_instantiate.argtypes = [ctypes.c_int, u32, u32, u32]
+    L.ref_destroy.argtypes = [vp]
+    L.ref_encode_batch_mt.restype = ctypes.c_double
+    L.ref_encode_batch_mt.argtypes = [vp, vp, vp, u32, u32, u32]
+    L.ref_decode_batch_mt.restype = ctypes.c_double
+    L.ref_decode_batch_mt.argtypes = [vp, vp, u32, ctypes.c_uint64, u32, u32]
+    return L
+
+
+def ref_baseline(fam, k, m, cs, threads, sample, run):
+    """Time the compiled reference on `sample` stripes: a single-worker
+    probe pass, then enough passes for ~10 s of CPU work (<= 4096).
+    run(L, h, passes, n_stripes, threads) -> seconds."""
+    L = _ref_lib()
+    if L is None or fam not in ("rs", "cauchy"):
+        return None
+    h = L.ref_instantiate(4 if fam == "rs" else 7, k, m, cs)  # CS_RS / CS_CAUCHY
+    if not h:
+        return None
+    try:
+        probe = run(L, h, 1, sample, 1)  # one worker, one pass over the sample
+        passes = int(max(1, min(4096, round(10.0 / max(probe, 1e-6)))))
+        dt = run(L, h, passes, sample, threads)
+    finally:
+        L.ref_destroy(h)
+    return probe, passes, dt
+
+
+def cpu_baseline_reference(fam, k, m, cs, gpu_parity_np, seed, threads, op, erased=None, codewords=None):
+    """kind "reference": MemEC's Coding::encode / Coding::decode themselves
+    (oracle/ref_shim.cc ref_*_batch_mt: worker threads on disjoint stripes,
+    chunks allocated once, as test/common/coding/batch_performance.cc runs
+    them).  The outputs are checked against the GPU's."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+
+    sample = decode_sample(k, m, cs, threads)
+    per = k * cs
+    if op == "encode":
+        data = O.fill(sample * per, seed)
+        par = np.zeros(sample * m * cs, np.uint8)
+
+        def run(L, h, passes, n, t):
+            return L.ref_encode_batch_mt(h, data.ctypes.data, par.ctypes.data, n, t, passes)
+    else:
+        present = sum(1 << i for i in range(k + m) if i not in erased)
+        buf = np.ascontiguousarray(codewords).reshape(-1).copy()
+
+        def run(L, h, passes, n, t):
+            return L.ref_decode_batch_mt(h, buf.ctypes.data, n, present, t, passes)
+    r = ref_baseline(fam, k, m, cs, threads, sample, run)
+    if r is None:
+        return None
+    probe, passes, dt = r
+    if dt < 0:
+        return {"error": "reference decode reported failure"}
+    if op == "encode":
+        match = None
+        if gpu_parity_np is not None:
+            n = min(sample, gpu_parity_np.shape[0])
+            match = bool((gpu_parity_np[:n].reshape(-1) == par[: n * m * cs]).all())
+    else:
+        match = bool(np.array_equal(buf.reshape(sample, k + m, cs), codewords))
+    return {"value": round(passes * sample * per / dt / 2**30, 4), "unit": "GiB/s", "cores": threads,
+            "kind": "reference",
+            "sample": "%d stripes x %d passes of the same workload%s through MemEC's own Coding::%s "
+                      "(common/coding + Jerasure + gf_complete compiled from the reference sources, "
+                      "oracle/_ref), %d worker threads on disjoint stripes as batch_performance.cc"
+                      % (sample, passes, "" if op == "encode" else ", erasures %s" % list(erased),
+                         "encode" if op == "encode" else "decode", threads),
+            "single_thread_value": round(sample * per / probe / 2**30, 4), "matches_gpu": match,
+            "cpu_model": cpu_model()}
+
+
 def decode_sample(k, m, cs, threads):
     sample = max(threads, min(64, (768 << 20) // ((k + m) * cs)))
     return (sample // threads) * threads or threads
@@ -439,11 +528,21 @@ def main():
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
             try:
                 if op == "encode":
-                    line["cpu_baseline"] = cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads)
+                    port = cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads)
                 elif op == "update":
-                    line["cpu_baseline"] = cpu_baseline_update(fam, k, m, cs, j, threads)
+                    port = cpu_baseline_update(fam, k, m, cs, j, threads)
                 else:
-                    line["cpu_baseline"] = cpu_baseline_decode(fam, k, m, cs, erased, codewords_np, threads)
+                    port = cpu_baseline_decode(fam, k, m, cs, erased, codewords_np, threads)
+                ref = None
+                if op != "update":  # the compiled reference itself, when oracle/_ref travelled
+                    ref = cpu_baseline_reference(fam, k, m, cs, gpu_parity_np if op == "encode" else None, seed,
+                                                 threads, op, erased, codewords_np if op == "decode" else None)
+                if ref and "error" not in ref:
+                    ref["port"] = {x: port[x] for x in ("value", "single_thread_value", "sample", "matches_gpu")
+                                   if x in port}
+                    line["cpu_baseline"] = ref
+                else:
+                    line["cpu_baseline"] = port
             except Exception as exc:  # report, never fake
                 line["cpu_baseline"] = {"error": repr(exc)}
         print(json.dumps(line), flush=True)

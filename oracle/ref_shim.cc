@@ -2,9 +2,11 @@
 //
 // TEST INFRASTRUCTURE ONLY.  Compiled by oracle/ref.mk against the reference
 // sources where they lie under /root/reference (nothing is copied into this
-// repo); the output goes to oracle/_ref/ (git-ignored).  Used only in this
+// repo); the output goes to oracle/_ref/ (git-ignored).  Used in this
 // container to generate tests/golden/ fixtures and to cross-check the C
-// restatement in oracle/oracle.c.  Never shipped, never built on the GPU box.
+// restatement in oracle/oracle.c, and (prebuilt, travelling with the tree)
+// by bench.py's cpu_baseline leg on the GPU box host.  Never built there,
+// never part of the product path.
 //
 // It drives MemEC's own plugin exactly as its test does
 // (test/common/coding/coding.cc:149-274): Coding::instantiate -> encode(index)
@@ -165,3 +167,104 @@ void ref_encode_chunks(void *hp, void *chunks, uint32_t first, uint32_t index) {
     h->coding->encode(c, c[h->k + index - 1], index);
 }
 }
+
+// Batch drivers for bench.py's cpu_baseline leg (kind "reference"): the
+// reference's own plugin run the way test/common/coding/batch_performance.cc
+// runs it (worker pthreads, chunks allocated once per worker, then a loop of
+// Coding calls on them), over disjoint stripe ranges.  Returns the wall time
+// in seconds of `passes` timed passes (setup and copies untimed), or < 0 on a
+// decode failure.
+//   encode: one Coding::encode(data, parity, 1) per stripe per pass — the
+//           plugin computes every parity of the stripe in that call
+//           (rscoding.cc:51-95, cauchycoding.cc:49-85); the remaining
+//           parities are then written out once, untimed, for verification.
+//   decode: one Coding::decode(chunks, status) per stripe per pass on the
+//           chunks whose present bit is clear (rebuilt in place).
+#include <atomic>
+#include <chrono>
+#include <thread>
+#include <vector>
+namespace {
+Chunk **stripes_in(const RefHandle *h, const uint8_t *src, uint32_t n) {
+    const uint32_t per = h->k + h->m;
+    Chunk **c = new Chunk *[(size_t)n * per];
+    TempChunkPool pool;
+    for (uint32_t s = 0; s < n; s++)
+        for (uint32_t i = 0; i < per; i++) {
+            c[(size_t)s * per + i] = pool.alloc();
+            if (src) memcpy(ChunkUtil::getData(c[(size_t)s * per + i]), src + ((size_t)s * per + i) * h->cs, h->cs);
+        }
+    return c;
+}
+void stripes_free(const RefHandle *h, Chunk **c, uint32_t n) {
+    TempChunkPool pool;
+    for (size_t i = 0; i < (size_t)n * (h->k + h->m); i++) pool.free(c[i]);
+    delete[] c;
+}
+template <typename F>
+double run_workers(uint32_t n, uint32_t threads, F body) {
+    std::vector<std::thread> th;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t t = 0; t < threads; t++)
+        th.emplace_back([=] { body((uint64_t)n * t / threads, (uint64_t)n * (t + 1) / threads); });
+    for (auto &x : th) x.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace
+extern "C" {
+// data: [n][k][cs] dense; parity: [n][m][cs] dense (written).
+double ref_encode_batch_mt(void *hp, const uint8_t *data, uint8_t *parity, uint32_t n, uint32_t threads,
+                           uint32_t passes) {
+    RefHandle *h = (RefHandle *)hp;
+    const uint32_t per = h->k + h->m;
+    std::vector<uint8_t> dense((size_t)n * per * h->cs, 0);
+    for (uint32_t s = 0; s < n; s++)
+        memcpy(&dense[(size_t)s * per * h->cs], data + (size_t)s * h->k * h->cs, (size_t)h->k * h->cs);
+    Chunk **c = stripes_in(h, dense.data(), n);
+    const double dt = run_workers(n, threads, [&](uint64_t a, uint64_t b) {
+        for (uint32_t p = 0; p < passes; p++)
+            for (uint64_t s = a; s < b; s++) {
+                Chunk **st = c + s * per;
+                h->coding->encode(st, st[h->k], 1);
+            }
+    });
+    run_workers(n, threads, [&](uint64_t a, uint64_t b) {  // untimed: the other parities
+        for (uint64_t s = a; s < b; s++)
+            for (uint32_t i = 2; i <= h->m; i++) h->coding->encode(c + s * per, c[s * per + h->k + i - 1], i);
+    });
+    for (uint32_t s = 0; s < n; s++) {
+        Chunk **st = c + (size_t)s * per;
+        for (uint32_t i = 0; i < h->m; i++)
+            memcpy(parity + ((size_t)s * h->m + i) * h->cs, ChunkUtil::getData(st[h->k + i]), h->cs);
+    }
+    stripes_free(h, c, n);
+    return dt;
+}
+
+// chunks: [n][k+m][cs] dense codewords; on return the erased chunks hold
+// the reference's reconstruction.
+double ref_decode_batch_mt(void *hp, uint8_t *chunks, uint32_t n, uint64_t present_mask, uint32_t threads,
+                           uint32_t passes) {
+    RefHandle *h = (RefHandle *)hp;
+    const uint32_t per = h->k + h->m;
+    Chunk **c = stripes_in(h, chunks, n);
+    for (uint32_t s = 0; s < n; s++)
+        for (uint32_t i = 0; i < per; i++)
+            if (!(present_mask >> i & 1)) memset(ChunkUtil::getData(c[(size_t)s * per + i]), 0, h->cs);
+    std::atomic<bool> all{true};
+    const double dt = run_workers(n, threads, [&](uint64_t a, uint64_t b) {
+        BitmaskArray bm(1, per);
+        for (uint32_t i = 0; i < per; i++)
+            if (present_mask >> i & 1) bm.set(i, 0);
+        bool good = true;
+        for (uint32_t p = 0; p < passes; p++)
+            for (uint64_t s = a; s < b; s++) good = h->coding->decode(c + s * per, &bm) && good;
+        if (!good) all = false;
+    });
+    for (uint32_t s = 0; s < n; s++)
+        for (uint32_t i = 0; i < per; i++)
+            memcpy(chunks + ((size_t)s * per + i) * h->cs, ChunkUtil::getData(c[(size_t)s * per + i]), h->cs);
+    stripes_free(h, c, n);
+    return all ? dt : -1.0;
+}
+}  // extern "C"
