@@ -401,6 +401,9 @@ def main():
         st = torch.empty(stripes, k + m, cs, dtype=torch.uint8, device=dev)
         st[:, :k] = data
         st[:, k:] = parity
+        dcodewords = None  # CPU-baseline sample of the twin: GPU-encoded codewords
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            dcodewords = st[:decode_sample(k, m, cs, args.cpu_threads or min(16, os.cpu_count() or 1))].cpu().numpy()
         saved = st[:, derased].clone()
         st[:, derased] = 0
         dpresent = sum(1 << i for i in range(k + m) if i not in derased)
@@ -537,6 +540,9 @@ def main():
                 if op != "update":  # the compiled reference itself, when oracle/_ref travelled
                     ref = cpu_baseline_reference(fam, k, m, cs, gpu_parity_np if op == "encode" else None, seed,
                                                  threads, op, erased, codewords_np if op == "decode" else None)
+                if secondary is not None and dcodewords is not None:  # the decode twin's reference
+                    secondary["cpu_baseline"] = cpu_baseline_reference(fam, k, m, cs, None, seed, threads, "decode",
+                                                                       secondary["erased"], dcodewords)
                 if ref and "error" not in ref:
                     ref["port"] = {x: port[x] for x in ("value", "single_thread_value", "sample", "matches_gpu")
                                    if x in port}
