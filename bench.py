@@ -35,7 +35,8 @@ CONFIGS = {
     "rs8_small": ("rs", 8, 2, 4096, 65536, "encode", None),                # configs[3]
     "crs_enc": ("cauchy", 12, 4, 65536, 4096, "encode", None),             # configs[4] per GPU
     "crs_dec": ("cauchy", 12, 4, 65536, 4096, "decode", [0, 1, 2, 3]),
-    "rs42": ("rs", 4, 2, 4096, 65536, "encode", None),
+    "rs42": ("rs", 4, 2, 4096, 65536, "encode", None),                    # configs[0] shape on the GPU
+    "rs42_dec": ("rs", 4, 2, 4096, 65536, "decode", [0, 1]),
     # the server's delta path (parity_chunk_buffer.cc:342-353): parity ^=
     # A[:, j] * delta for one data column j (last field = j)
     "rs8_update": ("rs", 8, 2, 4096, 65536, "update", 3),
@@ -48,7 +49,8 @@ WORKLOAD_NAMES = {
     "rs8_small": "RS(8,2) encode, 4 KiB chunks, 65536 stripes per GPU (configs[3])",
     "crs_enc": "Cauchy-RS(12,4) encode, 64 KiB chunks, 4096 stripes per GPU (configs[4] sharded)",
     "crs_dec": "Cauchy-RS(12,4) decode {0,1,2,3}, 64 KiB chunks, 4096 stripes per GPU",
-    "rs42": "RS(4,2) encode, 4 KiB chunks, 65536 stripes per GPU",
+    "rs42": "RS(4,2) encode, 4 KiB chunks, 65536 stripes per GPU (configs[0] shape)",
+    "rs42_dec": "RS(4,2) decode 2 erasures {0,1}, 4 KiB chunks, 65536 stripes per GPU (configs[0] shape)",
     "rs8_update": "RS(8,2) delta update of data column 3 into both parities, 4 KiB chunks, 65536 stripes per GPU",
     "rs_update": "RS(10,4) delta update of data column 3 into all 4 parities, 1 MiB chunks, 4096 stripes per GPU",
 }
@@ -395,7 +397,7 @@ def main():
     # twin (configs[2] for configs[1]) on the just-encoded stripes, every
     # rank, same barrier + max-over-ranks timing; reported beside `value`
     secondary = None
-    twin = {"rs_enc": "rs_dec", "crs_enc": "crs_dec"}.get(args.config)
+    twin = {"rs_enc": "rs_dec", "crs_enc": "crs_dec", "rs42": "rs42_dec"}.get(args.config)
     if op == "encode" and twin and not args.no_secondary:
         derased = CONFIGS[twin][6]
         st = torch.empty(stripes, k + m, cs, dtype=torch.uint8, device=dev)

@@ -34,7 +34,7 @@ for step in "$@"; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py ;;
         benchall)
-            for c in rs_enc rs_dec rs_dec_mixed rs8_small crs_enc crs_dec rs42; do
+            for c in rs_enc rs_dec rs_dec_mixed rs8_small crs_enc crs_dec rs42 rs42_dec; do
                 run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --steps 10
             done ;;
         batch) run bench_batch 600 python tools/bench_batch.py ;;
