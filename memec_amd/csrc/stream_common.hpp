@@ -121,11 +121,17 @@ inline Geometry geometry(uint64_t full_units, uint32_t threads = kThreads) {
 // RS(10,4)@1 MiB encode gains 1 %, RS(10,4) update 2.3 %, RS(8,2)@4 KiB
 // 2 %.  In-place layouts (win > 1) keep 4-wave blocks: one-wave blocks lose
 // 1.4 % (RS) to 5 % (CRS) on in-place decode
-// (profiles/r01/layout/block_ab*.log).  Returns kWaveBlock or kThreads (a
+// (profiles/r01/layout/block_ab*.log) — at RS(10,4)@1 MiB.  For byte-wise
+// (gf8) in-place layouts with stripes under kWaveBlockSpan bytes
+// (`small_span` = stripe stride; -1 = not applicable, the bitmatrix kernel)
+// one-wave blocks win instead: RS(4,2) / RS(10,4) in-place decode, chunks
+// 4 KiB-256 KiB, +2-7 points of HBM peak (tools/block_ab_sizes.py,
+// profiles/r01/layout/block_ab_sizes.log).  Returns kWaveBlock or kThreads (a
 // kernel template argument, so the 256-thread code is unchanged);
 // MEC_BLOCK=64|256 overrides it per launch (experiments).
 constexpr int kWaveBlock = 64;
-uint32_t block_threads(bool strided, uint32_t win);
+constexpr int64_t kWaveBlockSpan = int64_t(8) << 20;
+uint32_t block_threads(bool strided, uint32_t win, int64_t small_span = -1);
 
 }  // namespace detail
 }  // namespace mec

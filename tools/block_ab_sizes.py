@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Interleaved A/B of MEC_BLOCK=64 vs 256 for in-place RS decodes across
+chunk sizes (the block-size rule for in-place layouts).  ~4 GiB of stripe
+per case, 10 launches per sample, 5 rounds; median kernel ms.  Not product
+code."""
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from memec_amd import Codec, fill_random  # noqa: E402
+
+CASES = [("rs", 4, 2, [0, 1]), ("rs", 10, 4, [0, 1, 2, 3]), ("cauchy", 12, 4, [0, 1, 2, 3])]
+SIZES = [4096, 16384, 65536, 262144, 1 << 20]
+
+
+def main():
+    torch.cuda.set_device(0)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    for fam, k, m, erased in CASES:
+        for cs in SIZES:
+            n = max(1, (4 << 30) // ((k + m) * cs))
+            codec = Codec(fam, k, m, cs, device=0)
+            st = torch.empty(n, k + m, cs, dtype=torch.uint8, device="cuda")
+            fill_random(st, 1)
+            present = sum(1 << i for i in range(k + m) if i not in erased)
+            nbytes = (k + len(erased)) * cs * n
+            res = {64: [], 256: []}
+            for _ in range(5):
+                for b in (64, 256):
+                    os.environ["MEC_BLOCK"] = str(b)
+                    codec.decode(st, present)
+                    ev[0].record()
+                    for _ in range(10):
+                        codec.decode(st, present)
+                    ev[1].record()
+                    ev[1].synchronize()
+                    res[b].append(ev[0].elapsed_time(ev[1]) / 10)
+            os.environ.pop("MEC_BLOCK", None)
+            line = "%s(%d,%d) cs=%7d n=%6d" % (fam, k, m, cs, n)
+            for b in (64, 256):
+                med = statistics.median(res[b])
+                line += "  B%-3d %.4f ms %.1f%%" % (b, med, nbytes / med / 1e6 / 80)
+            print(line, flush=True)
+            del st
+            codec.close()
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
