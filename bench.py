@@ -126,6 +126,8 @@ def _ref_lib():
     L.ref_encode_batch_mt.argtypes = [vp, vp, vp, u32, u32, u32]
     L.ref_decode_batch_mt.restype = ctypes.c_double
     L.ref_decode_batch_mt.argtypes = [vp, vp, u32, ctypes.c_uint64, u32, u32]
+    L.ref_update_batch_mt.restype = ctypes.c_double
+    L.ref_update_batch_mt.argtypes = [vp, vp, vp, u32, u32, u32, u32]
     return L
 
 
@@ -192,6 +194,49 @@ def cpu_baseline_reference(fam, k, m, cs, gpu_parity_np, seed, threads, op, eras
                       % (sample, passes, "" if op == "encode" else ", erasures %s" % list(erased),
                          "encode" if op == "encode" else "decode", threads),
             "single_thread_value": round(sample * per / probe / 2**30, 4), "matches_gpu": match,
+            "cpu_model": cpu_model()}
+
+
+def cpu_baseline_reference_update(fam, k, m, cs, j, threads):
+    """kind "reference" for the delta path: MemEC's own calls as each parity
+    server makes them (parity_chunk_buffer.cc:342-353, 387-393) — per
+    stripe and parity index i, Coding::encode over Coding::zeros except
+    column j into a cleared chunk, then Coding::bitwiseXOR into parity i
+    (oracle/ref_shim.cc ref_update_batch_mt).  Checked against the oracle:
+    parity of (old data + delta) = old parity XOR parity delta (linearity)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+
+    sample = max(threads, min(256, (768 << 20) // ((k + 2 * m) * cs)))
+    sample = (sample // threads) * threads or threads
+    delta = O.fill(sample * cs, 5)
+    par0 = O.fill(sample * m * cs, 6)
+    par = par0.copy()
+
+    def run(L, h, passes, n, t):
+        return L.ref_update_batch_mt(h, delta.ctypes.data, par.ctypes.data, j, n, t, passes)
+    r = ref_baseline(fam, k, m, cs, threads, sample, run)
+    if r is None:
+        return None
+    probe, passes, dt = r
+    # every pass XORs the same parity delta: after 1 + passes applications the
+    # result is par0 ^ dpar (odd count) or par0 (even count)
+    dz = [np.zeros(cs, np.uint8)] * k
+    ok = True
+    for s_ in (0, sample - 1):
+        cols = list(dz)
+        cols[j] = delta[s_ * cs:(s_ + 1) * cs].copy()
+        dpar = np.stack(O.encode(fam, k, m, cols, cs)).reshape(-1)
+        want = par0[s_ * m * cs:(s_ + 1) * m * cs] ^ (dpar if (1 + passes) % 2 else 0)
+        ok = ok and bool(np.array_equal(par[s_ * m * cs:(s_ + 1) * m * cs], want))
+    return {"value": round(passes * sample * cs / dt / 2**30, 4), "unit": "GiB/s (delta bytes)", "cores": threads,
+            "kind": "reference",
+            "sample": "%d stripes x %d passes: per stripe and parity index, MemEC's own Coding::encode over "
+                      "Coding::zeros + the delta column into a cleared chunk, then Coding::bitwiseXOR into the "
+                      "parity, as each parity server runs it (oracle/_ref), %d worker threads"
+                      % (sample, passes, threads),
+            "single_thread_value": round(sample * cs / probe / 2**30, 4), "matches_oracle": ok,
             "cpu_model": cpu_model()}
 
 
@@ -538,8 +583,10 @@ def main():
                     port = cpu_baseline_update(fam, k, m, cs, j, threads)
                 else:
                     port = cpu_baseline_decode(fam, k, m, cs, erased, codewords_np, threads)
-                ref = None
-                if op != "update":  # the compiled reference itself, when oracle/_ref travelled
+                # the compiled reference itself, when oracle/_ref travelled
+                if op == "update":
+                    ref = cpu_baseline_reference_update(fam, k, m, cs, j, threads)
+                else:
                     ref = cpu_baseline_reference(fam, k, m, cs, gpu_parity_np if op == "encode" else None, seed,
                                                  threads, op, erased, codewords_np if op == "decode" else None)
                 if secondary is not None and dcodewords is not None:  # the decode twin's reference

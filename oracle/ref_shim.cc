@@ -267,4 +267,43 @@ double ref_decode_batch_mt(void *hp, uint8_t *chunks, uint32_t n, uint64_t prese
     stripes_free(h, c, n);
     return all ? dt : -1.0;
 }
+// delta: [n][cs] (one data column j per stripe); parity: [n][m][cs] in/out.
+// The server's delta path per stripe, as every parity server runs it
+// (parity_chunk_buffer.cc:342-353, 387-393): for each parity index i,
+// data = Coding::zeros except column j, ChunkUtil::clear(tmp),
+// Coding::encode(data, tmp, i), then parity_i ^= tmp (Coding::bitwiseXOR).
+double ref_update_batch_mt(void *hp, const uint8_t *delta, uint8_t *parity, uint32_t j, uint32_t n,
+                           uint32_t threads, uint32_t passes) {
+    RefHandle *h = (RefHandle *)hp;
+    const uint32_t per = h->k + h->m;
+    std::vector<uint8_t> dense((size_t)n * per * h->cs, 0);
+    for (uint32_t s = 0; s < n; s++) {
+        memcpy(&dense[((size_t)s * per + j) * h->cs], delta + (size_t)s * h->cs, h->cs);
+        memcpy(&dense[((size_t)s * per + h->k) * h->cs], parity + (size_t)s * h->m * h->cs, (size_t)h->m * h->cs);
+    }
+    Chunk **c = stripes_in(h, dense.data(), n);
+    const double dt = run_workers(n, threads, [&](uint64_t a, uint64_t b) {
+        TempChunkPool pool;
+        Chunk *tmp = pool.alloc();
+        Chunk *d[64];
+        for (uint32_t p = 0; p < passes; p++)
+            for (uint64_t s = a; s < b; s++) {
+                Chunk **st = c + s * per;
+                for (uint32_t x = 0; x < h->k; x++) d[x] = Coding::zeros;
+                d[j] = st[j];
+                for (uint32_t i = 1; i <= h->m; i++) {
+                    ChunkUtil::clear(tmp);
+                    h->coding->encode(d, tmp, i);
+                    char *par = ChunkUtil::getData(st[h->k + i - 1]);
+                    Coding::bitwiseXOR(par, par, ChunkUtil::getData(tmp), h->cs);
+                }
+            }
+        pool.free(tmp);
+    });
+    for (uint32_t s = 0; s < n; s++)
+        for (uint32_t i = 0; i < h->m; i++)
+            memcpy(parity + ((size_t)s * h->m + i) * h->cs, ChunkUtil::getData(c[(size_t)s * per + h->k + i]), h->cs);
+    stripes_free(h, c, n);
+    return dt;
+}
 }  // extern "C"

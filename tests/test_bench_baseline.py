@@ -68,3 +68,10 @@ def _fast(fn):
             return run(L, h, min(passes, 2), n, t)
         return fn(fam, k, m, cs, threads, sample, short_run)
     return wrapped
+
+
+@needs_ref
+def test_reference_update_leg(monkeypatch):
+    monkeypatch.setattr(bench, "ref_baseline", _fast(bench.ref_baseline))
+    r = bench.cpu_baseline_reference_update("rs", 4, 2, 4096, 1, 2)
+    assert r["kind"] == "reference" and r["matches_oracle"] is True and r["value"] > 0
