@@ -169,7 +169,8 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     p.s0 = 0;
     // block size from the whole launch's layout (sub-launches share it)
     const uint32_t bt = block_threads(!L.stab, L.stab ? 1u : launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride,
-                                                                          L.dst, int64_t(L.n_stripes) * L.dst_stripe_stride));
+                                                                          L.dst, int64_t(L.n_stripes) * L.dst_stripe_stride),
+                                      uint64_t(p.chunk) >= kBmWaveChunk);
     const Geometry g = geometry(L.packet / UB, bt);
     p.units = g.units;
     p.tiles = g.tiles;

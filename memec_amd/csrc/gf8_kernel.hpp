@@ -220,7 +220,7 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     // block size from the whole launch's layout (sub-launches share it)
     const uint32_t bt = block_threads(!L.stab, L.stab ? 1u : launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride,
                                                                           L.dst, int64_t(L.n_stripes) * L.dst_stripe_stride),
-                                      L.src_stripe_stride);
+                                      L.src_stripe_stride >= 0 && L.src_stripe_stride < kWaveBlockSpan);
     const Geometry g = geometry(L.len / 16, bt);
     p.units = g.units;
     p.tiles = g.tiles;

@@ -224,13 +224,13 @@ uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int6
     const int64_t a1 = a0 + std::max<int64_t>(src_span, 0), b1 = b0 + std::max<int64_t>(dst_span, 0);
     return (b0 < a1 && a0 < b1) ? 2u : 1u;
 }
-uint32_t block_threads(bool strided, uint32_t win, int64_t small_span) {
+uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place) {
     const char *e = std::getenv("MEC_BLOCK");  // read per launch: experiments flip it
     const int forced = e ? std::atoi(e) : 0;
     if (forced == kWaveBlock || forced == kThreads) return uint32_t(forced);
     if (!strided) return uint32_t(kThreads);
     if (win == 1) return uint32_t(kWaveBlock);
-    return small_span >= 0 && small_span < kWaveBlockSpan ? uint32_t(kWaveBlock) : uint32_t(kThreads);
+    return wave_in_place ? uint32_t(kWaveBlock) : uint32_t(kThreads);
 }
 }  // namespace detail
 

@@ -121,17 +121,21 @@ inline Geometry geometry(uint64_t full_units, uint32_t threads = kThreads) {
 // RS(10,4)@1 MiB encode gains 1 %, RS(10,4) update 2.3 %, RS(8,2)@4 KiB
 // 2 %.  In-place layouts (win > 1) keep 4-wave blocks: one-wave blocks lose
 // 1.4 % (RS) to 5 % (CRS) on in-place decode
-// (profiles/r01/layout/block_ab*.log) — at RS(10,4)@1 MiB.  For byte-wise
-// (gf8) in-place layouts with stripes under kWaveBlockSpan bytes
-// (`small_span` = stripe stride; -1 = not applicable, the bitmatrix kernel)
-// one-wave blocks win instead: RS(4,2) / RS(10,4) in-place decode, chunks
-// 4 KiB-256 KiB, +2-7 points of HBM peak (tools/block_ab_sizes.py,
-// profiles/r01/layout/block_ab_sizes.log).  Returns kWaveBlock or kThreads (a
-// kernel template argument, so the 256-thread code is unchanged);
-// MEC_BLOCK=64|256 overrides it per launch (experiments).
+// (profiles/r01/layout/block_ab*.log) — at RS(10,4)@1 MiB and
+// CRS(12,4)@64 KiB.  The chunk-size sweeps (tools/block_ab_sizes.py,
+// profiles/r01/layout/block_ab_sizes.log, block_ab_cauchy.log) find
+// in-place layouts where one-wave blocks win instead (`wave_in_place`):
+//   gf8 (byte-wise) with stripes under kWaveBlockSpan bytes: RS(4,2) /
+//     RS(10,4) in-place decode at 4 KiB-256 KiB chunks, +2-7 points;
+//   bitmatrix with chunks of kBmWaveChunk or more: CRS(12,4) / CRS(4,2)
+//     in-place decode at 256 KiB-2 MiB, +1-9 points (64 KiB keeps 4 waves:
+//     -6 points with one).
+// Returns kWaveBlock or kThreads (a kernel template argument, so the
+// 256-thread code is unchanged); MEC_BLOCK=64|256 overrides it per launch.
 constexpr int kWaveBlock = 64;
 constexpr int64_t kWaveBlockSpan = int64_t(8) << 20;
-uint32_t block_threads(bool strided, uint32_t win, int64_t small_span = -1);
+constexpr uint64_t kBmWaveChunk = uint64_t(256) << 10;
+uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place = false);
 
 }  // namespace detail
 }  // namespace mec

@@ -18,6 +18,10 @@ SIZES = [4096, 16384, 65536, 262144, 1 << 20]
 
 
 def main():
+    global CASES, SIZES
+    if os.environ.get("AB_CASES") == "cauchy":  # bitmatrix kernel, larger chunks
+        CASES = [("cauchy", 12, 4, [0, 1, 2, 3]), ("cauchy", 4, 2, [0, 1])]
+        SIZES = [65536, 131072, 262144, 524288, 1 << 20, 2 << 20]
     torch.cuda.set_device(0)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for fam, k, m, erased in CASES:
