@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of MEC_BLOCK=64 vs 256 for in-place RS decodes across
-chunk sizes (the block-size rule for in-place layouts).  ~4 GiB of stripe
+"""Interleaved A/B of MEC_BLOCK=64 vs 256 for in-place decodes (default) or
+split-buffer encodes (AB_OP=encode) across chunk sizes (the block-size
+rules).  ~4 GiB of stripe
 per case, 10 launches per sample, 5 rounds; median kernel ms.  Not product
 code."""
 import os
@@ -28,18 +29,31 @@ def main():
         for cs in SIZES:
             n = max(1, (4 << 30) // ((k + m) * cs))
             codec = Codec(fam, k, m, cs, device=0)
-            st = torch.empty(n, k + m, cs, dtype=torch.uint8, device="cuda")
-            fill_random(st, 1)
+            if os.environ.get("AB_OP") == "encode":  # split data / parity buffers
+                data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
+                fill_random(data, 1)
+                par = torch.empty(n, m, cs, dtype=torch.uint8, device="cuda")
+                st = (data, par)
+                nbytes = (k + m) * cs * n
+            else:
+                st = torch.empty(n, k + m, cs, dtype=torch.uint8, device="cuda")
+                fill_random(st, 1)
+                nbytes = (k + len(erased)) * cs * n
             present = sum(1 << i for i in range(k + m) if i not in erased)
-            nbytes = (k + len(erased)) * cs * n
+
+            def step():
+                if isinstance(st, tuple):
+                    codec.encode(*st)
+                else:
+                    codec.decode(st, present)
             res = {64: [], 256: []}
             for _ in range(5):
                 for b in (64, 256):
                     os.environ["MEC_BLOCK"] = str(b)
-                    codec.decode(st, present)
+                    step()
                     ev[0].record()
                     for _ in range(10):
-                        codec.decode(st, present)
+                        step()
                     ev[1].record()
                     ev[1].synchronize()
                     res[b].append(ev[0].elapsed_time(ev[1]) / 10)
