@@ -225,10 +225,11 @@ uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int6
     return (b0 < a1 && a0 < b1) ? 2u : 1u;
 }
 uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place) {
+    // gathered (pointer-table) launches are instantiated for kThreads only
+    if (!strided) return uint32_t(kThreads);
     const char *e = std::getenv("MEC_BLOCK");  // read per launch: experiments flip it
     const int forced = e ? std::atoi(e) : 0;
     if (forced == kWaveBlock || forced == kThreads) return uint32_t(forced);
-    if (!strided) return uint32_t(kThreads);
     if (win == 1) return uint32_t(kWaveBlock);
     return wave_in_place ? uint32_t(kWaveBlock) : uint32_t(kThreads);
 }

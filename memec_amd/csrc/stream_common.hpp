@@ -131,7 +131,9 @@ inline Geometry geometry(uint64_t full_units, uint32_t threads = kThreads) {
 //     in-place decode at 256 KiB-2 MiB, +1-9 points (64 KiB keeps 4 waves:
 //     -6 points with one).
 // Returns kWaveBlock or kThreads (a kernel template argument, so the
-// 256-thread code is unchanged); MEC_BLOCK=64|256 overrides it per launch.
+// 256-thread code is unchanged); MEC_BLOCK=64|256 overrides it per strided
+// launch (gathered launches always use kThreads: their kernels are only
+// instantiated for it).
 constexpr int kWaveBlock = 64;
 constexpr int64_t kWaveBlockSpan = int64_t(8) << 20;
 constexpr uint64_t kBmWaveChunk = uint64_t(256) << 10;
