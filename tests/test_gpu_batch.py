@@ -358,3 +358,24 @@ def test_update_batch_single_column(fam):
         want = O.encode(fam, k, m, list(d2), cs)
         for i in range(m):
             assert np.array_equal(got[s, i], want[i] if i != 1 else parity0[s, i]), (fam, s, i)
+
+
+@pytest.mark.parametrize("block", ["64", "256"])
+def test_block_override_every_launch_kind(block, monkeypatch):
+    """MEC_BLOCK (layout experiments) forces the block size of strided
+    launches and must leave results unchanged; gathered (pointer-table)
+    launches ignore it (their kernels exist for 256 threads only)."""
+    monkeypatch.setenv("MEC_BLOCK", block)
+    test_encode_batch_scattered("rs", "device", 8)
+    test_encode_batch_scattered("cauchy", "device", 8)
+    for fam in ("rs", "cauchy"):
+        k, m, cs, n = 6, 3, 4096, 24
+        c = Codec(fam, k, m, cs)
+        base = O.fill(n * (k + m) * cs, 555).reshape(n, k + m, cs)
+        for s in range(n):
+            base[s, k:] = np.stack(O.encode(fam, k, m, [base[s, j].copy() for j in range(k)], cs))
+        t = torch.from_numpy(base.copy()).to("cuda")
+        t[:, [0, 4, 7]] = 0
+        c.decode(t, sum(1 << i for i in range(k + m) if i not in (0, 4, 7)))
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), base), (fam, block)
