@@ -214,21 +214,24 @@ def cpu_baseline_reference_update(fam, k, m, cs, j, threads):
     par0 = O.fill(sample * m * cs, 6)
     par = par0.copy()
 
+    applied = np.zeros(sample, np.int64)  # delta applications per stripe, every call counted
+
     def run(L, h, passes, n, t):
+        applied[:n] += passes
         return L.ref_update_batch_mt(h, delta.ctypes.data, par.ctypes.data, j, n, t, passes)
     r = ref_baseline(fam, k, m, cs, threads, sample, run)
     if r is None:
         return None
     probe, passes, dt = r
-    # every pass XORs the same parity delta: after 1 + passes applications the
-    # result is par0 ^ dpar (odd count) or par0 (even count)
+    # every application XORs the same parity delta: an odd count leaves
+    # par0 ^ dpar, an even one par0
     dz = [np.zeros(cs, np.uint8)] * k
     ok = True
     for s_ in (0, sample - 1):
         cols = list(dz)
         cols[j] = delta[s_ * cs:(s_ + 1) * cs].copy()
         dpar = np.stack(O.encode(fam, k, m, cols, cs)).reshape(-1)
-        want = par0[s_ * m * cs:(s_ + 1) * m * cs] ^ (dpar if (1 + passes) % 2 else 0)
+        want = par0[s_ * m * cs:(s_ + 1) * m * cs] ^ (dpar if applied[s_] % 2 else 0)
         ok = ok and bool(np.array_equal(par[s_ * m * cs:(s_ + 1) * m * cs], want))
     return {"value": round(passes * sample * cs / dt / 2**30, 4), "unit": "GiB/s (delta bytes)", "cores": threads,
             "kind": "reference",
