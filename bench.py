@@ -143,7 +143,9 @@ def ref_baseline(fam, k, m, cs, threads, sample, run):
         return None
     try:
         probe = run(L, h, 1, sample, 1)  # one worker, one pass over the sample
-        passes = int(max(1, min(4096, round(10.0 / max(probe, 1e-6)))))
+        # >= 10 s of CPU work and >= ~2 s of wall time on `threads` workers
+        cpu_s = max(10.0, 2.0 * threads)
+        passes = int(max(1, min(4096, round(cpu_s / max(probe, 1e-6)))))
         dt = run(L, h, passes, sample, threads)
     finally:
         L.ref_destroy(h)
@@ -340,6 +342,60 @@ def load_traffic(cfg_name, stripes):
         return None
 
 
+def launcher_cmd(argv, gpus, port, python=None):
+    """The command that starts `gpus` rank processes of this script (one per
+    GPU) when bench.py is run as `python bench.py --gpus N` without a
+    launcher: torch.distributed.run on 127.0.0.1 with the same arguments.
+    The parent never touches the GPU; it waits and exits with the launcher's
+    status."""
+    return [python or sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            "--nproc-per-node=%d" % gpus, "--master-addr=127.0.0.1", "--master-port=%d" % port,
+            os.path.abspath(__file__)] + list(argv)
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(argv, gpus):
+    """Run the N-rank job as a child process (no exec: the parent has not
+    initialised the GPU, but a child keeps the rule simple) and return its
+    exit status."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(launcher_cmd(argv, gpus, _free_port()), env=env)
+
+
+def host_cores():
+    """CPU threads the CPU baseline may use on this host: the affinity mask,
+    capped by a cgroup CPU quota when one is set (the GPU box hands each GPU a
+    share of a larger machine, and nproc / os.cpu_count() show the whole
+    machine there).  Returns (threads, details)."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    threads = aff
+    if quota:
+        threads = max(1, min(aff, int(quota + 0.5)))
+    return threads, {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -357,14 +413,38 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory (PCIe) batch encode")
     ap.add_argument("--strong", action="store_true",
                     help="--stripes is the global batch, sharded over ranks (default: per-GPU batch, weak scaling)")
+    ap.add_argument("--dist-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    from memec_amd.shard import dist_env, max_over_ranks, shard_range, timed_steps
+
+    world, rank, local = dist_env()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N ranks
+        # before anything touches the GPU, wait, and return their status
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but the launcher started %d ranks" % (args.gpus, world))
 
     import torch
     import torch.distributed as dist
-    from memec_amd import Codec, fill_random
-    from memec_amd.shard import dist_env, shard_range, timed_steps
 
-    world, rank, local = dist_env()
+    if args.dist_check:  # launcher rehearsal without a GPU (tests/test_bench_launcher.py)
+        if world > 1:
+            dist.init_process_group("gloo")
+        ranks = [None] * world
+        if world > 1:
+            dist.all_gather_object(ranks, (rank, local, os.getpid()))
+            dist.destroy_process_group()
+        else:
+            ranks = [(rank, local, os.getpid())]
+        if rank == 0:
+            print(json.dumps({"dist_check": True, "n_gpus": args.gpus, "world_size": world, "ranks": ranks}),
+                  flush=True)
+        return
+
+    from memec_amd import Codec, fill_random
+
     # MEC_BENCH_DIST_BACKEND=gloo rehearses the multi-rank harness on fewer
     # GPUs than ranks (ranks share devices round-robin); the real run is
     # one rank per GPU over RCCL ("nccl").
@@ -373,11 +453,27 @@ def main():
         local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    dist_info = None
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit("bench.py: process group has %d ranks, --gpus %d"
+                             % (dist.get_world_size(), args.gpus))
+        devs = [None] * world
+        dist.all_gather_object(devs, local)
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(),
+                     "rccl": dist.get_backend() == "nccl", "rank_devices": devs}
+
+    def all_ranks_ok(flag):
+        """A verification holds only if it held on every rank."""
+        if world == 1:
+            return bool(flag)
+        bad = max_over_ranks([0.0 if flag else 1.0], dist,
+                             device="cpu" if dist.get_backend() == "gloo" else dev)
+        return bad[0] == 0.0
 
     fam, k, m, cs, stripes, op, erased = CONFIGS[args.config]
     if args.stripes:
@@ -421,7 +517,7 @@ def main():
         orig = stripe[:, erased].clone() if stripes * len(erased) * cs <= (24 << 30) else None
         codewords_np = None  # CPU-baseline sample: GPU-encoded stripes before the erasure
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            threads_cb = args.cpu_threads or min(16, os.cpu_count() or 1)
+            threads_cb = args.cpu_threads or host_cores()[0]
             codewords_np = stripe[:decode_sample(k, m, cs, threads_cb)].cpu().numpy()
         stripe[:, erased] = 0
 
@@ -453,7 +549,7 @@ def main():
         st[:, k:] = parity
         dcodewords = None  # CPU-baseline sample of the twin: GPU-encoded codewords
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            dcodewords = st[:decode_sample(k, m, cs, args.cpu_threads or min(16, os.cpu_count() or 1))].cpu().numpy()
+            dcodewords = st[:decode_sample(k, m, cs, args.cpu_threads or host_cores()[0])].cpu().numpy()
         saved = st[:, derased].clone()
         st[:, derased] = 0
         dpresent = sum(1 << i for i in range(k + m) if i not in derased)
@@ -466,7 +562,7 @@ def main():
                      "ms_per_step": round(dwall / args.steps * 1e3, 4), "kernel_ms": round(dkern, 4),
                      "achieved_GBps": round(dalg / (dkern * 1e-3) / 1e9, 1),
                      "frac": round(dalg / (dkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "verified": bool(torch.equal(st[:, derased], saved))}
+                     "verified": all_ranks_ok(torch.equal(st[:, derased], saved))}
         del st, saved
 
     ceiling = None
@@ -495,7 +591,7 @@ def main():
 
     ok = None
     if op == "decode" and orig is not None:
-        ok = bool(torch.equal(stripe[:, erased], orig))
+        ok = all_ranks_ok(torch.equal(stripe[:, erased], orig))
     if op == "update":
         # parity started as the parity of all-zero data and received the
         # same delta n times: it must equal the encode of (delta in column
@@ -506,7 +602,7 @@ def main():
             dz[:, j] = delta[:ref.shape[0]]
             codec.encode(dz, ref)
             del dz
-        ok = bool(torch.equal(parity[:ref.shape[0]], ref))
+        ok = all_ranks_ok(torch.equal(parity[:ref.shape[0]], ref))
         del ref
 
     gpu_parity_np = None
@@ -571,6 +667,8 @@ def main():
         }
         if ok is not None:
             line["decode_verified" if op == "decode" else "update_verified"] = ok
+        if dist_info:
+            line["dist"] = dist_info
         if e2e:
             line["e2e_host_memory"] = e2e
         if secondary:
@@ -578,7 +676,8 @@ def main():
             if ceiling:
                 secondary["frac_of_stream_ceiling"] = round(secondary["achieved_GBps"] / ceiling, 4)
         if not args.no_cpu_baseline and world == 1:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            threads, host = host_cores()
+            threads = args.cpu_threads or threads
             try:
                 if op == "encode":
                     port = cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads)
@@ -603,6 +702,9 @@ def main():
                     line["cpu_baseline"] = port
             except Exception as exc:  # report, never fake
                 line["cpu_baseline"] = {"error": repr(exc)}
+            for cb in (line["cpu_baseline"], (secondary or {}).get("cpu_baseline")):
+                if cb and "error" not in cb:
+                    cb["host"] = dict(host, threads_used=threads)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1,0 +1,44 @@
+"""`python bench.py --gpus 2` on the one-GPU box: the parent spawns two rank
+processes itself (no external launcher), both share cuda:0 over gloo
+(MEC_BENCH_DIST_BACKEND=gloo stands in for RCCL with fewer GPUs than
+ranks), and rank 0 prints one line with n_gpus 2, the process group's
+world size, and encode/decode output verified on every rank."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*extra):
+    env = dict(os.environ, MEC_BENCH_DIST_BACKEND="gloo")
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                          "--warmup", "1", "--no-ceiling", *extra],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_gpus2_spawns_ranks_weak():
+    rec = _run("--stripes", "64")
+    assert rec["n_gpus"] == 2
+    assert rec["dist"]["world_size"] == 2 and rec["dist"]["backend"] == "gloo"
+    assert rec["config"]["global_stripes"] == 128 and rec["config"]["stripes_per_gpu"] == 64
+    assert rec["decode"]["verified"] is True
+    assert rec["value"] > 0 and rec["roofline"]["kernel_ms"] > 0
+    assert rec["cpu_baseline"] is None  # rank 0 at N=1 only
+
+
+def test_bench_gpus2_strong_crs():
+    rec = _run("--config", "crs_enc", "--strong", "--stripes", "96")
+    assert rec["n_gpus"] == 2 and rec["scaling"] == "strong"
+    assert rec["config"]["global_stripes"] == 96 and rec["config"]["stripes_per_gpu"] == 48
+    assert rec["decode"]["verified"] is True
