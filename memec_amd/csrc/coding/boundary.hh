@@ -1,6 +1,6 @@
 // boundary.hh — the MemEC boundary types the Coding plugin touches
-// (SURVEY §8 a14).  Inside a MemEC tree (MEMEC_TREE defined, see
-// INTEGRATION.md) the real headers are used; standalone builds (tests, the
+// (SURVEY §8 a14).  Inside a MemEC tree (MEMEC_TREE: detected below, or
+// defined) the real headers are used; standalone builds (tests, the
 // GPU box) get these equivalents with the same layout and semantics:
 //   Chunk        char*: [8-byte ChunkIdentifier][chunkSize data bytes]
 //                (common/ds/chunk.hh:11-31)
@@ -10,11 +10,21 @@
 #ifndef MEMEC_AMD_CODING_BOUNDARY_HH
 #define MEMEC_AMD_CODING_BOUNDARY_HH
 
+// Inside a MemEC tree the adapter sits in common/coding/ next to ../ds/:
+// detect that, so the reference's own code (server/, the coding tests)
+// compiles against the adapter headers with its unchanged flags.
+#if !defined(MEMEC_TREE) && defined(__has_include)
+#if __has_include("../ds/chunk_util.hh")
+#define MEMEC_TREE 1
+#endif
+#endif
+
 #ifdef MEMEC_TREE
+// As the reference's coding.hh:4-7: only chunk.hh and bitmask_array.hh
+// here — ds/chunk_util.hh includes coding/coding.hh itself, so the
+// adapter's .cc files include chunk_util.hh / chunk_pool.hh (boundary_ds.hh).
 #include "../ds/bitmask_array.hh"
 #include "../ds/chunk.hh"
-#include "../ds/chunk_pool.hh"
-#include "../ds/chunk_util.hh"
 #else
 #include <stdint.h>
 #include <stdlib.h>

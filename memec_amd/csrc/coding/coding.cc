@@ -1,5 +1,5 @@
 // coding.cc — Coding factory and static helpers (common/coding/coding.cc).
-#include "coding.hh"
+#include "boundary_ds.hh"
 
 #include <stdio.h>
 #include <string.h>

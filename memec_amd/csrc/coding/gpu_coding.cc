@@ -1,5 +1,6 @@
 // gpu_coding.cc — RSCoding / CauchyCoding bodies over libmec.
 #include "gpu_coding.hh"
+#include "boundary_ds.hh"
 
 #include <stdio.h>
 #include <stdlib.h>
@@ -78,9 +79,11 @@ void GpuMatrixCoding::encode(Chunk **dataChunks, Chunk *parityChunk, uint32_t in
     uint8_t *parity[32] = {0};
     parity[index - 1] = (uint8_t *)ChunkUtil::getData(parityChunk);
     int rc;
-#ifdef USE_ISAL
-    if (startOff != 0 || endOff != 0) {
-        // ec_encode_data_update over the touched columns, XORed in place.
+    if (_family == MEC_ISAL_RS && (startOff != 0 || endOff != 0)) {
+        // USE_ISAL RSCoding: ec_encode_data_update over the touched columns,
+        // XORed in place (rscoding.cc:82-89).  USE_ISAL CauchyCoding ignores
+        // the offsets and overwrites with a full encode (cauchycoding.cc:78-79),
+        // as the Jerasure builds do (Appendix B #3).
         rc = MEC_OK;
         for (uint32_t i = startOff / _chunkSize; rc == MEC_OK && i <= (endOff - 1) / _chunkSize && i < _k; i++) {
             if (dataChunks[i] == Coding::zeros) continue;
@@ -89,10 +92,6 @@ void GpuMatrixCoding::encode(Chunk **dataChunks, Chunk *parityChunk, uint32_t in
         if (rc != MEC_OK) fprintf(stderr, "%s::encode: %s\n", _name, mec_last_error());
         return;
     }
-#else
-    (void)startOff;
-    (void)endOff;
-#endif
     const uint8_t *data[32];
     for (uint32_t j = 0; j < _k; j++)
         data[j] = dataChunks[j] == Coding::zeros ? 0 : (const uint8_t *)ChunkUtil::getData(dataChunks[j]);

@@ -113,7 +113,51 @@ static void *worker(void *p) {
     return 0;
 }
 
+// splitmix64 stream (oracle.c orc_fill_splitmix == mec_fill_random)
+static void fill_splitmix(char *buf, size_t n, uint64_t seed) {
+    for (size_t i = 0; i < n; i += 8) {
+        uint64_t z = seed + (i / 8 + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        for (size_t b = 0; b < 8 && i + b < n; b++) buf[i + b] = char(z >> (8 * b));
+    }
+}
+
+// coding_test encode-offsets <rs|cauchy> k m chunk index startOff endOff
+//                            data_seed parity_seed out.bin
+// One Coding::encode(data, parity, index, startOff, endOff) on a parity
+// chunk that already holds bytes (the server's delta call shape,
+// parity_chunk_buffer.cc:349-353); writes the parity chunk to out.bin.
+static int encode_offsets(int argc, char **argv) {
+    if (argc < 12) return 2;
+    CodingScheme scheme = strcmp(argv[2], "cauchy") == 0 ? CS_CAUCHY : CS_RS;
+    const uint32_t k = atoi(argv[3]), m = atoi(argv[4]), cs = atoi(argv[5]), index = atoi(argv[6]);
+    const uint32_t st = strtoul(argv[7], 0, 10), ed = strtoul(argv[8], 0, 10);
+    CodingParams params;
+    params.setScheme(scheme);
+    params.setK(k);
+    params.setM(m);
+    ChunkUtil::init(cs, k);
+    Coding *coding = Coding::instantiate(scheme, params, cs);
+    if (!coding) return 1;
+    {
+        Stripe s(k, m, cs);
+        std::vector<char> data(size_t(k) * cs);
+        fill_splitmix(data.data(), data.size(), strtoull(argv[9], 0, 10));
+        for (uint32_t j = 0; j < k; j++) memcpy(s.data(j), &data[size_t(j) * cs], cs);
+        fill_splitmix(s.data(k), cs, strtoull(argv[10], 0, 10));
+        coding->encode(&s.c[0], s.c[k], index, st, ed);
+        FILE *f = fopen(argv[11], "wb");
+        if (!f || fwrite(s.data(k), 1, cs, f) != cs) return 1;
+        fclose(f);
+    }
+    Coding::destroy(coding);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc > 1 && strcmp(argv[1], "encode-offsets") == 0) return encode_offsets(argc, argv);
     if (argc < 2) {
         fprintf(stderr, "usage: %s <rs|cauchy> [k m chunk]\n", argv[0]);
         return 2;
@@ -198,9 +242,11 @@ int main(int argc, char **argv) {
         Coding::bitwiseXOR(t.c[k + 1], d.c[k + 1], t.c[k + 1], cs);
         Stripe e(k, m, cs);
 #ifdef USE_ISAL
-        // ISA-L build: forceSeal's encode(..., 0, chunkSize) selects columns
+        // ISA-L RS: forceSeal's encode(..., 0, chunkSize) selects columns
         // [0, (chunkSize-1)/chunkSize] = {0} only (rscoding.cc:85-88); column
-        // 0 is Coding::zeros here, so the parity is left as it was.
+        // 0 is Coding::zeros here, so the parity is left as it was.  ISA-L
+        // Cauchy ignores the offsets (cauchycoding.cc:78-79).
+        if (scheme == CS_CAUCHY) coding->encode(&cols[0], e.c[k], 1);
 #else
         coding->encode(&cols[0], e.c[k], 1);  // chunk 2's term in parity 0
 #endif

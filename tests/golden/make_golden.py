@@ -35,6 +35,9 @@ REF.ref_destroy.argtypes = [ctypes.c_void_p]
 REF.ref_encode.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint32, ctypes.c_uint32, u8p]
 REF.ref_decode.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint64]
 REF.ref_isal_gf_mul.restype = ctypes.c_uint8
+REF.ref_isal_plugin_decode.restype = ctypes.c_int
+REF.ref_isal_plugin_decode.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(u8p), ctypes.c_ulonglong]
+REF.ref_isal_plugin_encode.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(u8p), u8p] + [ctypes.c_uint] * 3
 
 
 def fill(n, seed, word_offset=0):
@@ -255,6 +258,76 @@ def main():
                                    "delta_seed": s + 1, "column": col,
                                    "semantics": "parity (enc case) ^= coef[i][col] * delta"}
     meta["isal_matrices"] = isal
+
+    # --- ISA-L plugin decode (USE_ISAL RSCoding/CauchyCoding::decode) ----------------
+    # Random non-codeword stripes through the plugin's own steps
+    # (rscoding.cc:155-177, cauchycoding.cc:145-168; oracle/ref_isal_shim.c
+    # ref_isal_plugin_decode).  Erased DATA chunks are the reference's
+    # output.  For an erased PARITY chunk the plugin reads past the k x k
+    # inverse (uninitialised bytes; zero in the shim), so the fixture also
+    # holds `fixed`: the reference's own ISA-L encode (ref_isal_plugin_encode)
+    # of the data after the reference's decode — the value a correct decode
+    # writes there.
+    isal_dec = [
+        (4, 2, [[0], [1, 3], [0, 1], [4], [5], [4, 5], [0, 4], [3, 5]]),
+        (10, 4, [[0, 1, 2, 3], [0, 5, 9], [3], [9], [10], [13], [10, 11, 12, 13], [0, 5, 10, 13], [2, 7, 11],
+                 [9, 12]]),
+        (12, 4, [[0, 1, 2, 3], [11], [4, 8], [12], [15], [12, 13, 14, 15], [0, 5, 12, 15], [1, 14]]),
+        (6, 3, [[0, 1, 2], [5], [6], [8], [6, 7, 8], [0, 6], [2, 4, 8], [1, 7]]),
+    ]
+    cs = 256
+    for fam_i, fam in enumerate(("isal_rs", "isal_cauchy")):
+        for idx, (k, m, pats) in enumerate(isal_dec):
+            for p_i, pat in enumerate(pats):
+                s = seed + 5000 + 1000 * fam_i + 100 * idx + p_i
+                chunks = fill((k + m) * cs, s)
+                present = sum(1 << i for i in range(k + m) if i not in pat)
+                work = chunks.copy()
+                for e in pat:
+                    work[e * cs:(e + 1) * cs] = 0
+                cp = (u8p * (k + m))(*[ptr(work[i * cs:]) for i in range(k + m)])
+                rc = REF.ref_isal_plugin_decode(fam_i, k, m, cs, cp, present)
+                out = np.concatenate([work[e * cs:(e + 1) * cs] for e in sorted(pat)])
+                # reference re-encode of the decoded data -> correct parity
+                fixed = out.copy()
+                for r, e in enumerate(sorted(pat)):
+                    if e < k:
+                        continue
+                    dp = (u8p * k)(*[ptr(work[j * cs:]) for j in range(k)])
+                    par = np.zeros(cs, np.uint8)
+                    REF.ref_isal_plugin_encode(fam_i, k, m, cs, dp, ptr(par), e - k + 1, 0, 0)
+                    fixed[r * cs:(r + 1) * cs] = par
+                name = "dec/%s/%d_%d_%d/%s" % (fam, k, m, cs, "-".join(map(str, pat)))
+                blobs[name] = out
+                blobs[name + "|fixed"] = fixed
+                meta["cases"][name] = {"kind": "decode_random_isal", "family": fam, "k": k, "m": m, "chunk": cs,
+                                       "seed": s, "erased": pat, "rc": rc,
+                                       "input_layout": "[k+m][chunk] random; erased chunks cleared before decode",
+                                       "output_layout": "erased chunks ascending (reference plugin output)",
+                                       "fixed_layout": "same; erased parity replaced by the reference's ISA-L "
+                                                       "encode of the decoded data"}
+
+    # --- ISA-L plugin encode with startOff/endOff (the server's delta call) -------------
+    # RSCoding::encode's USE_ISAL update branch XORs ec_encode_data_update
+    # over data columns [startOff/chunk, (endOff-1)/chunk] into the caller's
+    # parity (rscoding.cc:82-89); CauchyCoding ignores the offsets and
+    # overwrites it with a full ec_encode_data (cauchycoding.cc:78-79).
+    for fam_i, fam in enumerate(("isal_rs", "isal_cauchy")):
+        for idx, (k, m, cs, index, st, ed) in enumerate([(10, 4, 512, 2, 3 * 512 + 100, 5 * 512 + 7),
+                                                        (4, 2, 4096, 1, 0, 4096), (6, 3, 256, 3, 1 * 256, 2 * 256),
+                                                        (12, 4, 512, 4, 11 * 512 + 1, 12 * 512)]):
+            s = seed + 7000 + 100 * fam_i + idx
+            data = fill(k * cs, s)
+            par = fill(cs, s + 1)
+            dp = (u8p * k)(*[ptr(data[j * cs:]) for j in range(k)])
+            REF.ref_isal_plugin_encode(fam_i, k, m, cs, dp, ptr(par), index, st, ed)
+            name = "encoff/%s/%d_%d_%d/i%d_s%d_e%d" % (fam, k, m, cs, index, st, ed)
+            blobs[name] = par
+            meta["cases"][name] = {"kind": "encode_offsets_isal", "family": fam, "k": k, "m": m, "chunk": cs,
+                                   "seed": s, "parity_seed": s + 1, "index": index, "startOff": st, "endOff": ed,
+                                   "data_layout": "[k][chunk] splitmix(seed)",
+                                   "parity_in": "[chunk] splitmix(parity_seed), the caller's parity chunk",
+                                   "expected": "the caller's parity chunk after RSCoding/CauchyCoding::encode"}
 
     np.savez_compressed(os.path.join(HERE, "golden.npz"), **{k.replace("/", "|"): v for k, v in blobs.items()})
     with open(os.path.join(HERE, "golden.json"), "w") as f:

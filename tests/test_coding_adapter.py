@@ -5,6 +5,7 @@ test flow) against the GPU (gpu)."""
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -62,3 +63,23 @@ def test_coding_flow_adapter_modes(binaries, env):
                                env=dict(os.environ, **env))
             assert r.returncode == 0, (b, args, env, r.stdout, r.stderr)
             assert ": ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_isal_encode_offsets_match_reference(binaries, golden, tmp_path):
+    """The USE_ISAL adapter's encode(data, parity, index, startOff, endOff)
+    on a parity chunk holding bytes, vs the reference plugin's steps
+    (tests/golden/make_golden.py: rscoding.cc:82-89 XORs
+    ec_encode_data_update_base over the touched columns; cauchycoding.cc:78-79
+    overwrites with a full encode)."""
+    meta, blobs = golden
+    cases = [(n, c) for n, c in sorted(meta["cases"].items()) if c["kind"] == "encode_offsets_isal"]
+    assert len(cases) == 8
+    isal_bin = binaries[1]
+    for name, c in cases:
+        out = tmp_path / "par.bin"
+        args = [isal_bin, "encode-offsets", "rs" if c["family"] == "isal_rs" else "cauchy"] + \
+            [str(c[x]) for x in ("k", "m", "chunk", "index", "startOff", "endOff", "seed", "parity_seed")] + [str(out)]
+        r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, (name, r.stdout, r.stderr)
+        assert np.array_equal(np.fromfile(str(out), dtype=np.uint8), blobs[name]), name

@@ -157,6 +157,34 @@ def test_decode_matches_reference_fixtures(golden):
                 assert np.array_equal(got[i], orig[i]), (name, i)
 
 
+def test_isal_decode_matches_reference_plugin(golden):
+    """USE_ISAL decode vs the reference plugin's own steps
+    (rscoding.cc:155-177, cauchycoding.cc:145-168 over ISA-L ec_base.c):
+    erased data chunks equal the reference's output; erased parity chunks
+    equal the reference's ISA-L encode of the decoded data (`fixed`) and
+    differ from the reference's output, which reads past the k x k inverse
+    (DESIGN §8)."""
+    meta, blobs = golden
+    cases = [(n, c) for n, c in sorted(meta["cases"].items()) if c["kind"] == "decode_random_isal"]
+    assert len(cases) >= 60
+    for name, c in cases:
+        k, m, cs = c["k"], c["m"], c["chunk"]
+        chunks = dev_fill((k + m) * cs, c["seed"]).view(1, k + m, cs).clone()
+        for e in c["erased"]:
+            chunks[0, e] = 0
+        present = sum(1 << i for i in range(k + m) if i not in c["erased"])
+        Codec(c["family"], k, m, cs).decode(chunks, present)
+        got = to_np(chunks)[0]
+        ref, fixed = blobs[name], blobs[name + "/fixed"]
+        for r, e in enumerate(sorted(c["erased"])):
+            assert np.array_equal(got[e], fixed[r * cs:(r + 1) * cs]), (name, e)
+            assert np.array_equal(got[e], ref[r * cs:(r + 1) * cs]) == (e < k), (name, e)
+        orig = O.fill((k + m) * cs, c["seed"]).reshape(k + m, cs)
+        for i in range(k + m):
+            if i not in c["erased"]:
+                assert np.array_equal(got[i], orig[i]), (name, i)
+
+
 @pytest.mark.parametrize("fam", ["rs", "cauchy", "isal_rs", "isal_cauchy"])
 def test_decode_every_pattern_vs_oracle(fam):
     """Every erasure pattern of size 1..m for (6,3), random stripes, against

@@ -139,6 +139,59 @@ def test_isal_matrices_and_update(golden):
         assert np.array_equal(base, blobs[name]), name
 
 
+def test_isal_plugin_decode_fixtures(golden):
+    """USE_ISAL decode, pinned on the reference plugin's own steps
+    (rscoding.cc:155-177, cauchycoding.cc:145-168 over ISA-L's ec_base.c):
+    every erased DATA chunk equals the reference's output bit for bit; an
+    erased PARITY chunk differs from it exactly there (the reference reads
+    rows of the k x k inverse past k) and equals `fixed`, the
+    reference's own ISA-L encode of the decoded data."""
+    meta, blobs = golden
+    cases = _encode_cases(meta, "decode_random_isal")
+    assert len(cases) >= 60
+    n_parity = 0
+    for name, c in cases:
+        k, m, cs = c["k"], c["m"], c["chunk"]
+        assert c["rc"] == 1, name
+        buf = O.fill((k + m) * cs, c["seed"])
+        chunks = [buf[i * cs:(i + 1) * cs].copy() for i in range(k + m)]
+        assert O.decode(c["family"], k, m, chunks, c["erased"], cs) == 0, name
+        ref, fixed = blobs[name], blobs[name + "/fixed"]
+        for r, e in enumerate(sorted(c["erased"])):
+            got = chunks[e]
+            assert np.array_equal(got, fixed[r * cs:(r + 1) * cs]), (name, e)
+            if e < k:
+                assert np.array_equal(got, ref[r * cs:(r + 1) * cs]), (name, e)
+            else:
+                n_parity += 1
+                assert not np.array_equal(got, ref[r * cs:(r + 1) * cs]), (name, e)
+    assert n_parity > 20
+
+
+def test_isal_plugin_encode_offsets_fixtures(golden):
+    """encode(..., index, startOff, endOff) of the USE_ISAL plugin: RS XORs
+    ec_encode_data_update over the touched columns into the caller's parity
+    (rscoding.cc:82-89); Cauchy ignores the offsets (cauchycoding.cc:78-79)."""
+    meta, blobs = golden
+    cases = _encode_cases(meta, "encode_offsets_isal")
+    assert len(cases) == 8
+    for name, c in cases:
+        k, m, cs, idx = c["k"], c["m"], c["chunk"], c["index"]
+        data = O.fill(k * cs, c["seed"])
+        cols = [data[j * cs:(j + 1) * cs].copy() for j in range(k)]
+        par = O.fill(cs, c["parity_seed"])
+        enc = O.isal_matrix(c["family"], k, m)
+        if c["family"] == "isal_rs":
+            coef = np.ascontiguousarray(enc[k * k:])
+            dst = [np.zeros(cs, np.uint8) for _ in range(m)]
+            dst[idx - 1] = par
+            for col in range(c["startOff"] // cs, (c["endOff"] - 1) // cs + 1):
+                O.lib().orc_isal_encode_update(cs, k, m, col, O.ptr(coef), O.ptr(cols[col]), O._ptrs(dst))
+        else:
+            par = O.encode(c["family"], k, m, cols, cs)[idx - 1]
+        assert np.array_equal(par, blobs[name]), name
+
+
 @pytest.mark.parametrize("fam", ["rs", "cauchy", "isal_rs", "isal_cauchy"])
 def test_roundtrip_every_pattern_small(fam):
     """encode -> erase -> decode restores the originals for every erasure
