@@ -89,14 +89,25 @@ void GpuMatrixCoding::encode(Chunk **dataChunks, Chunk *parityChunk, uint32_t in
             if (dataChunks[i] == Coding::zeros) continue;
             rc = mec_encode_update_host(_ctx, i, (const uint8_t *)ChunkUtil::getData(dataChunks[i]), parity);
         }
-        if (rc != MEC_OK) fprintf(stderr, "%s::encode: %s\n", _name, mec_last_error());
+        if (rc != MEC_OK) encode_failed(rc);
         return;
     }
     const uint8_t *data[32];
     for (uint32_t j = 0; j < _k; j++)
         data[j] = dataChunks[j] == Coding::zeros ? 0 : (const uint8_t *)ChunkUtil::getData(dataChunks[j]);
     rc = mec_encode_host(_ctx, data, parity);
-    if (rc != MEC_OK) fprintf(stderr, "%s::encode: %s\n", _name, mec_last_error());
+    if (rc != MEC_OK) encode_failed(rc);
+}
+
+// The reference's encode cannot fail (it returns void, rscoding.cc:51), so
+// its callers go on to XOR the parity into their buffers
+// (parity_chunk_buffer.cc:349-393).  libmec already retries on the launch
+// path when its queue fails; a call that still fails would leave stale
+// parity behind silently, so the process stops instead.
+void GpuMatrixCoding::encode_failed(int rc) const {
+    fprintf(stderr, "%s::encode: %s (rc %d); aborting rather than leaving parity unwritten\n", _name,
+            mec_last_error(), rc);
+    abort();
 }
 
 // rscoding.cc:97-187 / cauchycoding.cc:87-180.

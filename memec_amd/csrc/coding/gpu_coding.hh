@@ -25,6 +25,8 @@ protected:
     GpuMatrixCoding(int family, const char *name, uint32_t k, uint32_t m, uint32_t chunkSize);
 
 private:
+    void encode_failed(int rc) const;
+
     const char *_name;
     int _family;
     uint32_t _k, _m, _chunkSize;

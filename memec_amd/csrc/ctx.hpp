@@ -107,23 +107,31 @@ struct Coalescer {
 
 // queue.hip: device-side submission queue for single-stripe host calls.
 constexpr uint32_t kQMaxSrc = 32, kQMaxDst = 4, kQMaxSlots = 1024;
+constexpr uint32_t kQBmRows = kQMaxDst * 8;  // bitmatrix output packet rows (outputs x w <= 8)
 struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
     uint64_t seq;            // host -> GPU: number of the posted job
     uint64_t pad0[15];
     uint64_t done;           // GPU -> host: number of the last finished job
     uint64_t pad1[15];
-    uint32_t hdr[4];         // sources, outputs, chunk bytes, accumulate
+    // sources, outputs, chunk bytes, accumulate, w (0: byte-wise GF(2^8);
+    // 1..8: Jerasure bitmatrix over w packets), packet bytes, -, -
+    uint32_t hdr[8];
     uint64_t src[kQMaxSrc];  // device addresses of registered chunks (0 = zeros)
     uint64_t dst[kQMaxDst];  // (0 = unwanted output)
     uint32_t coef_w[kQMaxDst * kQMaxSrc / 4];  // GF(2^8) bytes, [output][source]
+    uint32_t mask_w[kQMaxSrc * kQBmRows / 4];  // bitmatrix bytes [source][output*w + l], bit x
 };
+// Grid-wide control words, after the slots in the same mapped allocation.
+enum : uint32_t { kQCtlStop = 0, kQCtlExit = 1, kQCtlWords = 2 };
 struct HostQueue {
     QSlot *host = nullptr, *dev = nullptr;
-    uint32_t *stop_host = nullptr, *stop_dev = nullptr;
+    uint32_t *ctl_host = nullptr, *ctl_dev = nullptr;  // [kQCtlStop] host -> GPU, [kQCtlExit] leader -> grid
+    uint64_t *act = nullptr;          // device memory: per-slot time of the last job (s_memrealtime)
     uint32_t slots = 0, max_chunk = 0, threads = 0;
     uint32_t solo_max = 0;            // larger chunks use the queue only beside other queue calls
     std::atomic<uint32_t> inflight{0};
-    uint64_t idle_ticks = 0;
+    std::atomic<bool> broken{false};  // a call timed out: the queue is stopped for good
+    uint64_t idle_ticks = 0, timeout_ms = 5000;
     std::atomic<bool> *busy = nullptr;
     hipStream_t stream = nullptr;
     std::mutex mu;  // launches
@@ -253,7 +261,8 @@ hipError_t lane_sync(hipStream_t s);
 
 // queue.hip.  queue_try: run one zero-copy call (addrs = ns sources then nd
 // outputs, device addresses) through the resident kernel; false = not
-// eligible or no free slot (nothing done), else rc holds the result.
+// eligible, no free slot, or a timed-out job that was withdrawn (nothing
+// done: the caller takes the launch path), else rc holds the result.
 bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Mat &coef, bool accumulate, int &rc);
 void queue_stop(mec_ctx *c);
 

@@ -17,17 +17,28 @@
 //     coefficients in LDS and codes the chunk over PCIe, one 16-byte unit
 //     per lane.
 // Exit conditions every wave reaches: the stop word (mec_set_host_queue(0),
-// mec_destroy) or an idle timeout measured with s_memrealtime.  A caller that
-// finds the kernel gone (idle exit) with its job pending relaunches it; the
-// new kernel starts from each slot's `done`, so no job is lost or run twice.
-// Launches of the resident kernel go to one stream, so two instances never
-// run at once.
+// mec_destroy, a timed-out call) or a grid-wide idle exit.  The idle exit is
+// decided for the whole grid at once: workgroup 0 (the leader) watches every
+// slot's last-activity time and, when no slot has had work for
+// MEC_QUEUE_IDLE_MS, sets the exit word that every workgroup polls.  So the
+// grid always leaves together and the stream completes: a caller whose job
+// is still pending then relaunches the kernel (queue_revive), which starts
+// from each slot's `done`, so no job is lost or run twice.  (A per-workgroup
+// idle timer would let one slot's workgroup leave while others keep the
+// stream busy, stranding calls posted to that slot.)  Launches of the
+// resident kernel go to one stream, so two instances never run at once.
 //
-// Scope: byte-wise families (RS, ISA-L), chunks of at most
-// MEC_QUEUE_MAX_CHUNK bytes (default 16 KiB; larger chunks want the whole
-// GPU, so they keep the launch path), either zero-copy (registered) or
-// staged: unregistered chunks are copied into a lane's mapped pinned buffer
-// and the workgroup codes that buffer in place (mec.cpp lane_run).
+// A call that sees no completion within MEC_QUEUE_TIMEOUT_MS (5 s) withdraws its job (its
+// sequence number moves back), stops the queue for good and waits for the
+// grid to leave; if its job never ran, the caller codes it on the launch
+// path instead (queue_try returns false).
+//
+// Scope: chunks of at most MEC_QUEUE_MAX_CHUNK bytes (default 16 KiB;
+// larger chunks want the whole GPU, so they keep the launch path), either
+// zero-copy (registered) or staged (mec.cpp lane_run), for every family:
+// byte-wise GF(2^8) products (RS, ISA-L) and the Jerasure Cauchy bitmatrix
+// over w packets of chunk/w bytes (cauchycoding.cc:80), whose masks the
+// caller expands from the GF(2^w) coefficients.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -43,6 +54,7 @@ namespace mec {
 namespace core {
 namespace {
 
+using detail::u32x2;
 using detail::u32x4;
 constexpr int kQThreads = 1024;  // most threads per slot: a 16 KiB chunk in one pass
 constexpr int kQBatch = 16;
@@ -127,72 +139,195 @@ __device__ __forceinline__ void code_unit(const uint64_t *addr, const uint32_t *
     }
 }
 
+// ---- bitmatrix (Jerasure Cauchy-RS) jobs --------------------------------
+// acc ^= d & m as one v_bitop3_b32 (truth table 0x6A), as bm_kernel.hpp.
+__device__ __forceinline__ u32x2 bm_axor(u32x2 d, uint32_t m, u32x2 acc) {
+    return u32x2{uint32_t(__builtin_amdgcn_bitop3_b32(d.x, m, acc.x, 0x6A)),
+                 uint32_t(__builtin_amdgcn_bitop3_b32(d.y, m, acc.y, 0x6A))};
+}
+
+__device__ __forceinline__ u32x2 ld8(uint64_t p, uint32_t n) {
+    if (n == 8) return *reinterpret_cast<const u32x2 *>(p);
+    const uint8_t *b = reinterpret_cast<const uint8_t *>(p);
+    uint32_t w[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (uint32_t(i) < n) w[i / 4] |= uint32_t(b[i]) << (8 * (i % 4));
+    return u32x2{w[0], w[1]};
+}
+
+__device__ __forceinline__ void st8(uint64_t p, u32x2 v, uint32_t n) {
+    if (n == 8) {
+        *reinterpret_cast<u32x2 *>(p) = v;
+        return;
+    }
+    uint8_t *b = reinterpret_cast<uint8_t *>(p);
+    const uint32_t w[2] = {v.x, v.y};
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        if (uint32_t(i) < n) b[i] = uint8_t(w[i / 4] >> (8 * (i % 4)));
+}
+
+// The n-byte slice (n <= 8) at offset off of every packet: output packet
+// (r, l) (^)= XOR over (j, x) with bit x of mk[j][r*W + l] of source packet
+// (j, x) (jerasure_do_scheduled_operations' result, jerasure.c:1162-1185).
+// Sources are loaded B at a time (B*W slices in flight, one PCIe round trip).
+template <int W>
+__device__ __forceinline__ void bm_unit(const uint64_t *addr, const uint8_t *mk, uint32_t ns, uint32_t nd,
+                                        uint32_t acc_in, uint64_t off, uint32_t n, uint64_t P) {
+    constexpr int B = W >= 16 ? 1 : 16 / W;
+    u32x2 acc[kQMaxDst * W];
+#pragma unroll
+    for (int r = 0; r < int(kQMaxDst); ++r) {
+        const uint64_t d = addr[kQMaxSrc + r];
+#pragma unroll
+        for (int l = 0; l < W; ++l)
+            acc[r * W + l] = (acc_in && uint32_t(r) < nd && d) ? ld8(d + l * P + off, n) : u32x2{0, 0};
+    }
+    for (uint32_t j0 = 0; j0 < ns; j0 += B) {
+        u32x2 x[B][W];
+#pragma unroll
+        for (int jj = 0; jj < B; ++jj) {
+            const uint64_t a = j0 + jj < ns ? addr[j0 + jj] : 0;  // 0: Coding::zeros / past ns
+#pragma unroll
+            for (int xw = 0; xw < W; ++xw) x[jj][xw] = a ? ld8(a + xw * P + off, n) : u32x2{0, 0};
+        }
+#pragma unroll
+        for (int jj = 0; jj < B; ++jj) {
+            if (j0 + jj >= ns) break;
+            const uint8_t *mb = mk + (j0 + jj) * kQBmRows;
+#pragma unroll
+            for (int r = 0; r < int(kQMaxDst); ++r) {
+                if (uint32_t(r) >= nd) break;
+#pragma unroll
+                for (int l = 0; l < W; ++l) {
+                    const uint32_t bits = mb[r * W + l];
+#pragma unroll
+                    for (int xw = 0; xw < W; ++xw)
+                        acc[r * W + l] = bm_axor(x[jj][xw], 0u - ((bits >> xw) & 1u), acc[r * W + l]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < int(kQMaxDst); ++r) {
+        const uint64_t d = addr[kQMaxSrc + r];
+        if (uint32_t(r) >= nd || !d) continue;
+#pragma unroll
+        for (int l = 0; l < W; ++l) st8(d + l * P + off, acc[r * W + l], n);
+    }
+}
+
+template <int W>
+__device__ __forceinline__ void bm_job(const uint64_t *addr, const uint8_t *mk, uint32_t ns, uint32_t nd,
+                                       uint32_t acc_in, uint32_t P, uint32_t t, uint32_t nthr) {
+    const uint32_t units = (P + 7) / 8;
+    for (uint32_t u = t; u < units; u += nthr) {
+        const uint32_t off = u * 8;
+        bm_unit<W>(addr, mk, ns, nd, acc_in, off, P - off < 8 ? P - off : 8, P);
+    }
+}
+
 template <typename T>
 __device__ __forceinline__ T sys_load(const T *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, const uint32_t *stop, uint64_t idle_ticks,
-                                                         uint32_t nthr) {
+__device__ __forceinline__ void mark_active(uint64_t *act) {
+    __hip_atomic_store(act, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr uint32_t kQDescWords = 8 + 2 * (kQMaxSrc + kQMaxDst) + kQMaxDst * kQMaxSrc / 4 + kQMaxSrc * kQBmRows / 4;
+
+__global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t *ctl, uint64_t *act,
+                                                         uint64_t idle_ticks, uint32_t nthr, uint32_t nslots) {
+    __shared__ uint32_t desc[kQDescWords];  // the slot's descriptor: hdr, src, dst, coef_w, mask_w
     __shared__ uint32_t tab[kQMaxDst * kQMaxSrc * 8];
-    __shared__ uint64_t addr[kQMaxSrc + kQMaxDst];
-    __shared__ uint32_t hdr[4];
-    __shared__ uint32_t cw[kQMaxDst * kQMaxSrc / 4];
     __shared__ uint32_t cmd;
     QSlot *s = slots + blockIdx.x;
     const uint32_t t = threadIdx.x;
+    const bool leader = blockIdx.x == 0;
     uint64_t last = 0, t0 = 0;
     if (t == 0) {
         last = sys_load(&s->done);
         t0 = __builtin_amdgcn_s_memrealtime();
     }
+    const uint32_t *hdr = desc;
+    const uint64_t *addr = reinterpret_cast<const uint64_t *>(desc + 8);
+    const uint32_t *cw = desc + 8 + 2 * (kQMaxSrc + kQMaxDst);
+    const uint8_t *mk = reinterpret_cast<const uint8_t *>(cw + kQMaxDst * kQMaxSrc / 4);
     for (;;) {
         if (t == 0) {
             uint32_t c = 0;
-            for (uint32_t n = 1;; ++n) {  // one PCIe read per poll; stop / idle every 64th
+            for (uint32_t n = 1;; ++n) {  // one PCIe read per poll; control words every 64th
                 const uint64_t q = __hip_atomic_load(&s->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (q != last) {
+                if (q > last) {  // a withdrawn job moves seq back (queue_try)
                     last = q;
                     c = 1;
                     break;
                 }
-                if (n % 64 == 0 &&
-                    (sys_load(stop) != 0u || __builtin_amdgcn_s_memrealtime() - t0 > idle_ticks))
-                    break;
+                if (n % 64 == 0) {
+                    if ((sys_load(ctl + kQCtlStop) | sys_load(ctl + kQCtlExit)) != 0u) break;
+                    if (leader) {  // grid-wide idle: no slot has worked for idle_ticks
+                        uint64_t newest = t0;
+                        for (uint32_t i = 0; i < nslots; ++i) {
+                            const uint64_t a = __hip_atomic_load(act + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            newest = a > newest ? a : newest;
+                        }
+                        if (__builtin_amdgcn_s_memrealtime() - newest > idle_ticks) {
+                            __hip_atomic_store(ctl + kQCtlExit, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            break;
+                        }
+                    }
+                }
                 __builtin_amdgcn_s_sleep(4);
             }
             cmd = c;
+            if (c) mark_active(act + blockIdx.x);
         }
         __syncthreads();
-        if (cmd == 0) return;  // uniform: stop or idle
-        if (t < 4) hdr[t] = sys_load(&s->hdr[t]);
-        if (t < kQMaxSrc) addr[t] = sys_load(&s->src[t]);
-        else if (t < kQMaxSrc + kQMaxDst) addr[t] = sys_load(&s->dst[t - kQMaxSrc]);
-        else if (t < kQMaxSrc + kQMaxDst + kQMaxDst * kQMaxSrc / 4)
-            cw[t - kQMaxSrc - kQMaxDst] = sys_load(&s->coef_w[t - kQMaxSrc - kQMaxDst]);
-        __syncthreads();
-        const uint32_t ns = hdr[0], nd = hdr[1], bytes = hdr[2], acc_in = hdr[3];
-        if (t < nd * ns) {
-            const uint32_t r = t / ns, j = t - r * ns, b = r * kQMaxSrc + j;
-            const uint32_t c = (cw[b / 4] >> (8 * (b % 4))) & 0xffu;
-            uint32_t *T = tab + b * 8;
-            T[0] = pack4(c, 0, 1, 2, 3);
-            T[1] = pack4(c, 4, 5, 6, 7);
-            T[2] = pack4(c, 0, 8, 16, 24);
-            T[3] = pack4(c, 32, 40, 48, 56);
-            T[4] = pack4(c, 0, 64, 128, 192);
+        if (cmd == 0) return;  // uniform: stop or grid idle
+        {  // descriptor: hdr, src, dst as 32-bit words, coefficients, masks
+            const uint32_t *sw = reinterpret_cast<const uint32_t *>(&s->hdr[0]);
+            for (uint32_t i = t; i < kQDescWords; i += nthr) desc[i] = sys_load(sw + i);
         }
         __syncthreads();
-        const uint32_t full = bytes / 16;
-        for (uint32_t u = t; u < full; u += nthr)
-            code_unit<true>(addr, tab, ns, nd, acc_in, uint64_t(u) * 16, 16);
-        if (bytes % 16 && t == full % nthr)  // the partial last unit
-            code_unit<false>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
+        const uint32_t ns = hdr[0], nd = hdr[1], bytes = hdr[2], acc_in = hdr[3], w = hdr[4], P = hdr[5];
+        if (w == 0) {  // byte-wise GF(2^8): v_perm tables from the coefficient bytes
+            if (t < nd * ns) {
+                const uint32_t r = t / ns, j = t - r * ns, b = r * kQMaxSrc + j;
+                const uint32_t c = (cw[b / 4] >> (8 * (b % 4))) & 0xffu;
+                uint32_t *T = tab + b * 8;
+                T[0] = pack4(c, 0, 1, 2, 3);
+                T[1] = pack4(c, 4, 5, 6, 7);
+                T[2] = pack4(c, 0, 8, 16, 24);
+                T[3] = pack4(c, 32, 40, 48, 56);
+                T[4] = pack4(c, 0, 64, 128, 192);
+            }
+            __syncthreads();
+            const uint32_t full = bytes / 16;
+            for (uint32_t u = t; u < full; u += nthr)
+                code_unit<true>(addr, tab, ns, nd, acc_in, uint64_t(u) * 16, 16);
+            if (bytes % 16 && t == full % nthr)  // the partial last unit
+                code_unit<false>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
+        } else {
+            switch (w) {  // uniform
+                case 1: bm_job<1>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
+                case 2: bm_job<2>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
+                case 3: bm_job<3>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
+                case 4: bm_job<4>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
+                case 5: bm_job<5>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
+                case 6: bm_job<6>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
+                case 7: bm_job<7>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
+                case 8: bm_job<8>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
+                default: break;
+            }
+        }
         __threadfence_system();  // this lane's outputs reach host memory ...
         __syncthreads();         // ... before the slot is marked done
         if (t == 0) {
             __hip_atomic_store(&s->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            t0 = __builtin_amdgcn_s_memrealtime();
+            mark_active(act + blockIdx.x);
         }
     }
 }
@@ -202,23 +337,38 @@ uint64_t env_u64(const char *name, uint64_t dflt) {
     return e && *e ? std::strtoull(e, nullptr, 10) : dflt;
 }
 
-// Launch the resident kernel (caller holds q->mu).
+// Launch the resident kernel (caller holds q->mu; no instance is running).
 int queue_launch(mec_ctx *c, HostQueue *q) {
     DeviceGuard dg(c->device);
-    hipLaunchKernelGGL(queue_kernel, dim3(q->slots), dim3(q->threads), 0, q->stream, q->dev, q->stop_dev, q->idle_ticks,
-                       q->threads);
+    __atomic_store_n(q->ctl_host + kQCtlExit, 0u, __ATOMIC_RELEASE);
+    hipLaunchKernelGGL(queue_kernel, dim3(q->slots), dim3(q->threads), 0, q->stream, q->dev, q->ctl_dev, q->act,
+                       q->idle_ticks, q->threads, q->slots);
     HIP_TRY(hipGetLastError());
     q->launches++;
     return MEC_OK;
 }
 
-// The resident kernel has exited (idle) while jobs may be pending: relaunch.
+// The resident grid has exited (idle) while jobs may be pending: relaunch.
+// While it is still leaving (the exit word reaches every workgroup within
+// one poll interval) the stream is busy and the caller retries.
 int queue_revive(mec_ctx *c, HostQueue *q) {
     std::lock_guard<std::mutex> g(q->mu);
+    if (q->broken.load()) return fail(MEC_EHIP, "host queue stopped after a timed-out call");
     const hipError_t e = hipStreamQuery(q->stream);
     if (e == hipErrorNotReady) return MEC_OK;  // still running
     if (e != hipSuccess) return hip_fail(e, "queue kernel");
     return queue_launch(c, q);
+}
+
+// Wait up to `ms` for the resident grid to leave; true once it has.
+bool queue_drained(HostQueue *q, int ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(ms)) {
+        const hipError_t e = hipStreamQuery(q->stream);
+        if (e != hipErrorNotReady) return e == hipSuccess;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    return false;
 }
 
 }  // namespace
@@ -229,10 +379,11 @@ void queue_stop(mec_ctx *c) {
     c->hq = nullptr;
     {
         DeviceGuard dg(c->device);
-        __atomic_store_n(q->stop_host, 1u, __ATOMIC_RELEASE);
+        __atomic_store_n(q->ctl_host + kQCtlStop, 1u, __ATOMIC_RELEASE);
         (void)hipStreamSynchronize(q->stream);  // every workgroup sees the stop word and returns
         (void)hipStreamDestroy(q->stream);
         (void)hipHostFree(q->host);
+        (void)hipFree(q->act);
     }
     delete[] q->busy;
     delete q;
@@ -242,34 +393,48 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     if (slots > kQMaxSlots) return fail(MEC_EINVAL, "at most %u queue slots", kQMaxSlots);
     DeviceGuard dg(c->device);
     std::unique_ptr<HostQueue> q(new HostQueue);
-    q->slots = slots;
     q->max_chunk = uint32_t(env_u64("MEC_QUEUE_MAX_CHUNK", 16 << 10));
     // a lone call on a chunk above this codes faster as a launch (many
     // workgroups over PCIe) than on one queue workgroup
     q->solo_max = uint32_t(env_u64("MEC_QUEUE_SOLO_MAX", q->max_chunk));
     q->idle_ticks = env_u64("MEC_QUEUE_IDLE_MS", 50) * 100000ull;  // s_memrealtime: 100 MHz
+    q->timeout_ms = env_u64("MEC_QUEUE_TIMEOUT_MS", 5000);
     // one 16-byte unit per thread up to kQThreads (a 4 KiB chunk: 256 threads;
     // idle threads only cost barrier time), at least 128 (descriptor loads)
     q->threads = std::min<uint32_t>(kQThreads, std::max<uint32_t>(128, (c->cs / 16 + 63) / 64 * 64));
+    // every slot's workgroup must be resident at once: a slot whose
+    // workgroup waits for another to exit would never be served
+    {
+        int per_cu = 0, cus = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_kernel, int(q->threads), 0));
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+        const uint32_t cap = uint32_t(std::max(1, per_cu * cus));
+        slots = std::min(slots, cap);
+    }
+    q->slots = slots;
     const size_t bytes = sizeof(QSlot) * slots + 256;
     void *h = nullptr;
     HIP_TRY(hipHostMalloc(&h, bytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable));
     std::memset(h, 0, bytes);
     void *d = nullptr;
     hipError_t e = hipHostGetDevicePointer(&d, h, 0);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&q->act), sizeof(uint64_t) * slots);
+    if (e == hipSuccess) e = hipMemset(q->act, 0, sizeof(uint64_t) * slots);
     if (e != hipSuccess) {
         (void)hipHostFree(h);
-        return hip_fail(e, "hipHostGetDevicePointer");
+        if (q->act) (void)hipFree(q->act);
+        return hip_fail(e, "queue memory");
     }
     q->host = static_cast<QSlot *>(h);
     q->dev = static_cast<QSlot *>(d);
-    q->stop_host = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(h) + sizeof(QSlot) * slots);
-    q->stop_dev = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d) + sizeof(QSlot) * slots);
+    q->ctl_host = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(h) + sizeof(QSlot) * slots);
+    q->ctl_dev = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d) + sizeof(QSlot) * slots);
     q->busy = new std::atomic<bool>[slots];
     for (uint32_t i = 0; i < slots; ++i) q->busy[i].store(false);
     e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         (void)hipHostFree(h);
+        (void)hipFree(q->act);
         delete[] q->busy;
         return hip_fail(e, "hipStreamCreate");
     }
@@ -279,6 +444,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
         if (rc != MEC_OK) {
             (void)hipStreamDestroy(q->stream);
             (void)hipHostFree(h);
+            (void)hipFree(q->act);
             delete[] q->busy;
             return rc;
         }
@@ -289,7 +455,8 @@ int queue_start(mec_ctx *c, uint32_t slots) {
 
 bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Mat &coef, bool accumulate, int &rc) {
     HostQueue *q = c->hq;
-    if (!q || !c->byte_wise() || c->cs > q->max_chunk || ns > kQMaxSrc || nd > kQMaxDst || nd == 0)
+    if (!q || q->broken.load(std::memory_order_relaxed) || c->cs > q->max_chunk || ns > kQMaxSrc ||
+        nd > kQMaxDst || nd == 0 || (!c->byte_wise() && (c->w < 1 || c->w > 8)))
         return false;
     if (c->cs > q->solo_max && q->inflight.load(std::memory_order_relaxed) == 0) return false;
     // a free slot, starting from a per-thread hint so callers spread out
@@ -309,37 +476,67 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     s->hdr[1] = uint32_t(nd);
     s->hdr[2] = c->cs;
     s->hdr[3] = accumulate ? 1u : 0u;
+    s->hdr[4] = c->byte_wise() ? 0u : c->w;
+    s->hdr[5] = c->byte_wise() ? c->cs : c->packet;
     for (size_t j = 0; j < ns; ++j) s->src[j] = addrs[j];
     for (size_t r = 0; r < nd; ++r) s->dst[r] = addrs[ns + r];
-    uint8_t cb[kQMaxDst * kQMaxSrc] = {};
-    for (size_t r = 0; r < nd; ++r)
-        for (size_t j = 0; j < ns; ++j) cb[r * kQMaxSrc + j] = coef[r * ns + j];
-    std::memcpy(s->coef_w, cb, sizeof(cb));
+    if (c->byte_wise()) {
+        uint8_t cb[kQMaxDst * kQMaxSrc] = {};
+        for (size_t r = 0; r < nd; ++r)
+            for (size_t j = 0; j < ns; ++j) cb[r * kQMaxSrc + j] = coef[r * ns + j];
+        std::memcpy(s->coef_w, cb, sizeof(cb));
+    } else {  // GF(2^w) coefficients -> bitmatrix rows (jerasure_matrix_to_bitmatrix)
+        const Field &f = Field::get(int(c->w));
+        uint8_t mk[kQMaxSrc][kQBmRows] = {};
+        for (size_t r = 0; r < nd; ++r)
+            for (size_t j = 0; j < ns; ++j) bit_block(f, coef[r * ns + j], c->w, &mk[j][r * c->w], 1);
+        std::memcpy(s->mask_w, mk, sizeof(mk));
+    }
     const uint64_t seq = __atomic_load_n(&s->seq, __ATOMIC_RELAXED) + 1;
     __atomic_store_n(&s->seq, seq, __ATOMIC_RELEASE);  // publishes the descriptor
-    // wait for the workgroup; relaunch the kernel if it idled out meanwhile
+    // wait for the workgroup; relaunch the grid if it idled out meanwhile
     rc = MEC_OK;
+    bool taken = true;
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t spins = 0;
     while (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != seq) {
-        if (++spins % 2048 == 0) {
+        if (++spins % 2048 == 0 || q->timeout_ms == 0) {
             const auto dt = std::chrono::steady_clock::now() - t0;
-            if (dt > std::chrono::seconds(5)) {
-                rc = fail(MEC_EHIP, "host queue: no completion within 5 s");
-                break;  // the slot stays busy: its job may still run
+            if (dt > std::chrono::milliseconds(q->timeout_ms) || q->broken.load()) {
+                // Withdraw the job (seq moves back: a workgroup that has not
+                // taken it never will, one that has runs the unchanged
+                // descriptor to the end), stop the queue for good, and wait
+                // for the grid to leave.  Then done == seq means the job ran;
+                // otherwise nothing can touch the caller's chunks any more and
+                // the launch path codes them instead.
+                rc = MEC_OK;
+                __atomic_store_n(&s->seq, seq - 1, __ATOMIC_SEQ_CST);
+                q->broken.store(true);
+                __atomic_store_n(q->ctl_host + kQCtlStop, 1u, __ATOMIC_RELEASE);
+                const bool drained = queue_drained(q, 1000);
+                if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == seq) break;  // it ran after all
+                if (drained) {
+                    taken = false;
+                } else {
+                    rc = fail(MEC_EHIP, "host queue: no completion within %llu ms and the grid did not stop",
+                              (unsigned long long)q->timeout_ms);
+                }
+                break;
             }
             if (dt > std::chrono::microseconds(200)) std::this_thread::yield();
-            rc = queue_revive(c, q);
-            if (rc != MEC_OK) break;
+            if (queue_revive(c, q) != MEC_OK && !q->broken.load()) {
+                rc = MEC_EHIP;  // the relaunch failed (error text set); the job is withdrawn below
+                q->broken.store(true);
+            }
         }
         __builtin_ia32_pause();
     }
     q->inflight.fetch_sub(1, std::memory_order_relaxed);
-    if (rc == MEC_OK) {
+    if (rc == MEC_OK && taken) {
         q->busy[i].store(false, std::memory_order_release);
         q->calls++;
     }
-    return true;
+    return taken;
 }
 
 }  // namespace core
@@ -355,6 +552,7 @@ int mec_set_host_queue(mec_ctx *c, uint32_t slots) {
         int rc = mec_set_host_queue(s, slots);
         if (rc != MEC_OK) return rc;
     }
+    if (!c->shards.empty()) return MEC_OK;  // a multi-device context's host calls all go to its shards
     std::lock_guard<std::mutex> g(c->hq_mu);
     queue_stop(c);
     return slots ? queue_start(c, slots) : MEC_OK;

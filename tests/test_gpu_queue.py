@@ -4,8 +4,11 @@ posted to a resident kernel instead of launched.  Bit-exact against the
 oracle for encode(index) / decode / delta update, under concurrent callers
 (MemEC's workers share one Coding, worker.cc:128-137), across an idle exit
 and relaunch, and with the launch path taking what the queue does not serve
-(bitmatrix Cauchy, chunks above MEC_QUEUE_MAX_CHUNK, queue stopped).
-Unregistered (staged) chunks reach the queue through mapped pinned lanes.
+(chunks above MEC_QUEUE_MAX_CHUNK, queue stopped).  Jerasure Cauchy-RS
+(bitmatrix over w packets) is served too.  Unregistered (staged) chunks
+reach the queue through mapped pinned lanes.  The grid-wide idle exit keeps
+a caller on a quiet slot from stranding while another slot stays busy, and
+a timed-out call withdraws its job and falls back to the launch path.
 """
 import ctypes
 import os
@@ -25,6 +28,7 @@ from memec_amd._lib import check, lib  # noqa: E402
 
 vp = ctypes.c_void_p
 BYTEWISE = ["rs", "isal_rs", "isal_cauchy"]
+FAMILIES = BYTEWISE + ["cauchy"]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -69,9 +73,21 @@ def encode_index(c, slab, k, dslots, pslot, index):
     check(lib().mec_encode_host(c._h, dp, pp))
 
 
-@pytest.mark.parametrize("fam", BYTEWISE)
+@pytest.mark.parametrize("fam", FAMILIES)
 @pytest.mark.parametrize("k,m,cs", [(8, 2, 4096), (10, 4, 16384), (4, 2, 4104), (12, 4, 1024), (20, 4, 2048)])
 def test_queue_encode_decode_update(fam, k, m, cs):
+    """Cauchy w: 4 (packets of 1 KiB, 4 KiB, 256 B), 3 (1368 B), 8 (256 B)."""
+    _encode_decode_update(fam, k, m, cs)
+
+
+@pytest.mark.parametrize("k,m,cs", [(4, 2, 4100), (3, 1, 24), (12, 4, 16376), (6, 3, 4104)])
+def test_queue_cauchy_packet_tails(k, m, cs):
+    """Bitmatrix packets that are not whole 8-byte units: w=4 / 1025 B,
+    w=2 / 12 B, w=4 / 4094 B, w=4 / 1026 B."""
+    _encode_decode_update("cauchy", k, m, cs)
+
+
+def _encode_decode_update(fam, k, m, cs):
     slab = Slab(k + m + 1, cs, 31 + k)
     c = Codec(fam, k, m, cs)
     try:
@@ -174,22 +190,90 @@ def test_queue_idle_exit_and_relaunch():
         slab.close()
 
 
+def test_queue_quiet_slot_beside_busy_slot():
+    """one caller keeps a slot busy while a second caller
+    posts to another slot only every few idle periods.  The idle exit is
+    grid-wide, so the quiet caller is never left waiting on a workgroup that
+    has left while the rest of the grid keeps the stream busy."""
+    k, m, cs = 8, 2, 4096
+    os.environ["MEC_QUEUE_IDLE_MS"] = "5"
+    slab = Slab(2 * (k + m), cs, 77)
+    c = Codec("rs", k, m, cs)
+    stop = threading.Event()
+    errs, slow = [], []
+    try:
+        c.set_host_queue(2)
+        wants = [O.encode("rs", k, m, [slab.view(b + j).copy() for j in range(k)], cs) for b in (0, k + m)]
+
+        def busy():
+            try:
+                while not stop.is_set():
+                    slab.view(k)[:] = 0
+                    encode_index(c, slab, k, list(range(k)), k, 1)
+                    if not np.array_equal(slab.view(k), wants[0][0]):
+                        errs.append("busy")
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+        th = threading.Thread(target=busy)
+        th.start()
+        b = k + m
+        for rnd in range(12):
+            time.sleep(0.02)  # 4 idle periods of the quiet slot
+            slab.view(b + k + 1)[:] = 0
+            t0 = time.perf_counter()
+            encode_index(c, slab, k, [b + j for j in range(k)], b + k + 1, 2)
+            dt = time.perf_counter() - t0
+            if dt > 0.5:
+                slow.append((rnd, dt))
+            assert np.array_equal(slab.view(b + k + 1), wants[1][1]), rnd
+        stop.set()
+        th.join()
+        assert not errs, errs[:5]
+        assert not slow, slow
+    finally:
+        stop.set()
+        os.environ.pop("MEC_QUEUE_IDLE_MS", None)
+        c.close()
+        slab.close()
+
+
+@pytest.mark.parametrize("fam", ["rs", "cauchy"])
+def test_queue_timeout_withdraws_and_falls_back(fam):
+    """a call that sees no completion in time withdraws
+    its job, stops the queue for good and — when the job never ran — codes
+    on the launch path.  MEC_QUEUE_TIMEOUT_MS=0 makes the first call time
+    out at once; every result stays exact, and later calls use launches."""
+    k, m, cs = 6, 3, 4096
+    os.environ["MEC_QUEUE_TIMEOUT_MS"] = "0"
+    slab = Slab(k + m, cs, 91)
+    c = Codec(fam, k, m, cs)
+    try:
+        c.set_host_queue(4)
+        want = O.encode(fam, k, m, [slab.view(j).copy() for j in range(k)], cs)
+        for rnd in range(3):
+            for i in range(m):
+                slab.view(k + i)[:] = 0
+                encode_index(c, slab, k, list(range(k)), k + i, i + 1)
+                assert np.array_equal(slab.view(k + i), want[i]), (rnd, i)
+        st = c.stats()
+        assert st["queue_calls"] <= 1  # at most the first call, if it beat the withdrawal
+        assert st["zero_copy_calls"] == 3 * m
+        # staged calls on the broken queue take launches too
+        data = [O.fill(cs, 300 + j) for j in range(k)]
+        got = c.encode_host(data)
+        w2 = O.encode(fam, k, m, [d.copy() for d in data], cs)
+        for i in range(m):
+            assert np.array_equal(got[i], w2[i])
+    finally:
+        os.environ.pop("MEC_QUEUE_TIMEOUT_MS", None)
+        c.close()
+        slab.close()
+
+
 def test_queue_fallbacks():
     """Calls the queue does not serve still code correctly through launches."""
     k, m = 4, 2
-    # bitmatrix Cauchy: not byte-wise
-    slab = Slab(k + m, 4096, 3)
-    c = Codec("cauchy", k, m, 4096)
-    try:
-        c.set_host_queue(4)
-        want = O.encode("cauchy", k, m, [slab.view(j).copy() for j in range(k)], 4096)
-        encode_index(c, slab, k, list(range(k)), k, 1)
-        assert np.array_equal(slab.view(k), want[0])
-        st = c.stats()
-        assert st["queue_calls"] == 0 and st["zero_copy_calls"] == 1
-    finally:
-        c.close()
-        slab.close()
     # chunk above MEC_QUEUE_MAX_CHUNK, then the queue stopped
     cs = 128 << 10
     slab = Slab(k + m, cs, 4)
@@ -223,7 +307,7 @@ def test_queue_fallbacks():
         c.close()
 
 
-@pytest.mark.parametrize("fam", BYTEWISE)
+@pytest.mark.parametrize("fam", FAMILIES)
 @pytest.mark.parametrize("k,m,cs", [(8, 2, 4096), (10, 4, 16384), (4, 2, 4104), (20, 4, 2048)])
 def test_queue_staged_calls(fam, k, m, cs):
     """Unregistered host chunks go through a lane's mapped pinned buffer to
