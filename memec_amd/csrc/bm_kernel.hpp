@@ -191,10 +191,11 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
+                const uint32_t lds = occupancy_lds(bt, std::min<uint32_t>(bt, g.units), 0, bm_target_waves(R));
                 if (bt == kWaveBlock)
-                    hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
+                    hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
                 else
-                    hipLaunchKernelGGL((bm_kernel<W, R, false, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
+                    hipLaunchKernelGGL((bm_kernel<W, R, false, kThreads>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
             }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;

@@ -19,6 +19,7 @@
 //  * xor_kernel — region XOR (Coding::bitwiseXOR, coding.cc:88-118).
 //  * fill_kernel — splitmix64 fill for synthetic stripes.
 #include <array>
+#include <cmath>
 #include <cstdlib>
 #include <utility>
 
@@ -232,6 +233,30 @@ uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place) {
     if (forced == kWaveBlock || forced == kThreads) return uint32_t(forced);
     if (win == 1) return uint32_t(kWaveBlock);
     return wave_in_place ? uint32_t(kWaveBlock) : uint32_t(kThreads);
+}
+namespace {
+uint32_t ceil_even(double x) { return 2u * uint32_t(std::ceil(x / 2.0)); }
+uint32_t clampw(uint32_t w, uint32_t lo, uint32_t hi) { return std::min(hi, std::max(lo, w)); }
+}  // namespace
+
+uint32_t gf8_target_waves(int k, int rows, bool in_place) {
+    const double w = 64.0 / std::max(1, k) + (in_place ? 2.0 : 1.0) * rows;
+    return in_place ? clampw(ceil_even(w), 8, 24) : clampw(ceil_even(w), 6, 20);
+}
+
+uint32_t bm_target_waves(int rows) { return clampw(uint32_t(3 * rows), 6, 16); }
+
+uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32_t waves) {
+    const char *e = std::getenv("MEC_WPC");  // read per launch: experiments flip it
+    if (e) waves = uint32_t(std::max(0, std::atoi(e)));
+    if (waves == 0) return 0;
+    constexpr uint32_t kLdsPerCu = 160u << 10, kGranule = 512;
+    const uint32_t per = std::max<uint32_t>(1, std::min(bt, std::max<uint32_t>(active, 1)) / 64 +
+                                                   (std::min(bt, std::max<uint32_t>(active, 1)) % 64 ? 1 : 0));
+    const uint32_t blocks = std::max<uint32_t>(1, (waves + per - 1) / per);
+    const uint32_t per_block = kLdsPerCu / blocks / kGranule * kGranule;
+    const uint32_t used = (static_lds + kGranule - 1) / kGranule * kGranule;
+    return per_block > used + kGranule ? per_block - used - kGranule : 0;
 }
 }  // namespace detail
 

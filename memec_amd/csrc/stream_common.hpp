@@ -139,5 +139,25 @@ constexpr int64_t kWaveBlockSpan = int64_t(8) << 20;
 constexpr uint64_t kBmWaveChunk = uint64_t(256) << 10;
 uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place = false);
 
+// Resident waves per CU of a streaming launch, capped through the LDS each
+// block reserves (the kernels themselves use only their small coefficient
+// tables).  More waves than the memory system can keep streaming cost HBM
+// throughput: uncapped, the gf8 kernels run 79-84 % of 8 TB/s wherever
+// their VGPR budget puts occupancy, capped at the right count 82-87 %
+// (tools/wpc_ab.py, profiles/r02/wpc/).  The right count falls as a wave's
+// own in-flight reads grow and rises with its output streams:
+//   gf8 (all K source loads of a wave in flight at once)
+//     split outputs (encode, update):  ceil_even(64 / K + R),  6..20
+//     in place (decode):               ceil_even(64 / K + 2R), 8..24
+//   bitmatrix (one source, W packets, prefetched one ahead): 3R, 6..16
+// in active waves (waves that own units; a block of small packets can have
+// idle ones).  MEC_WPC=<n> overrides (0 = no cap): experiments flip it.
+uint32_t gf8_target_waves(int k, int rows, bool in_place);
+uint32_t bm_target_waves(int rows);
+// Dynamic LDS bytes per block of `bt` threads (`active` of them owning
+// units, `static_lds` bytes of static LDS) so that about `waves` active waves
+// share a CU; 0 = no cap.
+uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32_t waves);
+
 }  // namespace detail
 }  // namespace mec
