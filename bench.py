@@ -569,8 +569,8 @@ def main():
     if rank == 0 and not args.no_ceiling:
         # on-box streaming ceiling: libmec's plain region XOR
         # (Coding::bitwiseXOR; 2 non-temporal 16-B reads + 1 write per lane,
-        # no arithmetic to speak of) over 3 x 8 GiB, best of 5 — the same
-        # access shape as the coding kernels.  (torch's own copy kernel
+        # no arithmetic to speak of) over 3 x 8 GiB, best of 15 launches
+        # over 5 occupancy caps — the same access shape as the coding kernels.  (torch's own copy kernel
         # reaches only ~4.6-5.0 TB/s here, tools/ceil_probe.py.)
         from memec_amd import xor as mec_xor
         a = torch.empty(8 << 30, dtype=torch.uint8, device=dev)
@@ -578,14 +578,25 @@ def main():
         out = torch.empty_like(a)
         mec_xor(out, a, b)
         best = None
-        for _ in range(5):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            mec_xor(out, a, b)
-            e1.record()
-            e1.synchronize()
-            ms = e0.elapsed_time(e1)
-            best = ms if best is None else min(best, ms)
+        # the stream's own best occupancy: its default cap and a few others
+        # (MEC_WPC, memec_amd/csrc/stream_common.hpp)
+        saved = os.environ.pop("MEC_WPC", None)
+        for wpc in (None, "0", "12", "16", "24"):
+            if wpc is None:
+                os.environ.pop("MEC_WPC", None)
+            else:
+                os.environ["MEC_WPC"] = wpc
+            for _ in range(3):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                mec_xor(out, a, b)
+                e1.record()
+                e1.synchronize()
+                ms = e0.elapsed_time(e1)
+                best = ms if best is None else min(best, ms)
+        os.environ.pop("MEC_WPC", None)
+        if saved is not None:
+            os.environ["MEC_WPC"] = saved
         ceiling = 3 * a.numel() / (best * 1e-3) / 1e9
         del a, b, out
 

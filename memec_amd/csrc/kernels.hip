@@ -249,7 +249,10 @@ uint32_t bm_target_waves(int rows) { return clampw(uint32_t(3 * rows), 6, 16); }
 uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32_t waves) {
     const char *e = std::getenv("MEC_WPC");  // read per launch: experiments flip it
     if (e) waves = uint32_t(std::max(0, std::atoi(e)));
-    if (waves == 0) return 0;
+    // a block with less than one wave's worth of units streams too little
+    // per wave for a cap to pay (CRS at 2 KiB chunks: 75 % uncapped, 51 %
+    // capped, profiles/r02/sweep)
+    if (waves == 0 || (!e && active < 64)) return 0;
     constexpr uint32_t kLdsPerCu = 160u << 10, kGranule = 512;
     const uint32_t per = std::max<uint32_t>(1, std::min(bt, std::max<uint32_t>(active, 1)) / 64 +
                                                    (std::min(bt, std::max<uint32_t>(active, 1)) % 64 ? 1 : 0));
@@ -387,7 +390,9 @@ hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream) {
 hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, hipStream_t stream) {
     if (len == 0) return hipSuccess;
     const uint64_t units = (len + 15) / 16, blocks = (units + kThreads - 1) / kThreads;
-    hipLaunchKernelGGL(xor_kernel, dim3(uint32_t(std::min<uint64_t>(blocks, uint64_t(1) << 22))), dim3(kThreads), 0,
+    // 2 source streams + 1 output per lane: the gf8 split-layout rule
+    const uint32_t lds = occupancy_lds(kThreads, kThreads, 0, gf8_target_waves(2, 1, false));
+    hipLaunchKernelGGL(xor_kernel, dim3(uint32_t(std::min<uint64_t>(blocks, uint64_t(1) << 22))), dim3(kThreads), lds,
                        stream, dst, a, b, len);
     return hipGetLastError();
 }

@@ -26,6 +26,7 @@ if os.environ.get("WPC_CASES"):  # fam:k:m,...
     CASES = [(c.split(":")[0], int(c.split(":")[1]), int(c.split(":")[2])) for c in os.environ["WPC_CASES"].split(",")]
 if os.environ.get("WPC_LIST"):
     WPC = [int(x) for x in os.environ["WPC_LIST"].split(",")]
+VAR = os.environ.get("WPC_VAR", "MEC_WPC")  # the knob swept (e.g. MEC_WINDOWS); 0 = unset
 
 
 def main():
@@ -55,7 +56,10 @@ def main():
                 res = {w: [] for w in WPC}
                 for _ in range(5):
                     for w in WPC:
-                        os.environ["MEC_WPC"] = str(w)
+                        if VAR != "MEC_WPC" and w == 0:
+                            os.environ.pop(VAR, None)
+                        else:
+                            os.environ[VAR] = str(w)
                         step()
                         ev[0].record()
                         for _ in range(8):
@@ -63,7 +67,7 @@ def main():
                         ev[1].record()
                         ev[1].synchronize()
                         res[w].append(ev[0].elapsed_time(ev[1]) / 8)
-                os.environ.pop("MEC_WPC", None)
+                os.environ.pop(VAR, None)
                 pct = {w: nbytes / (statistics.median(v) * 1e-3) / 8e12 * 100 for w, v in res.items()}
                 best = max(pct, key=pct.get)
                 print("%-6s %-6s k=%-2d m=%d cs=%-7d " % (op, fam, k, m, cs) +
