@@ -218,9 +218,15 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     p.chunk = uint32_t(L.len);
     p.s0 = 0;
     // block size from the whole launch's layout (sub-launches share it)
+    // one-wave blocks in place only for stripe strides under kWaveBlockSpan
+    // that are not a power of two: a 512 KiB / 1 MiB stride with one-wave
+    // blocks decodes at 62-71 % of 8 TB/s, with 4-wave blocks at 77-82 %
+    // (tools/wpc_ab.py WPC_VAR=MEC_BLOCK, profiles/r02/wpc/win_pow2.log)
+    const int64_t sss = L.src_stripe_stride;
+    const bool wave_ok = sss >= 0 && sss < kWaveBlockSpan && (sss & (sss - 1)) != 0;
     const uint32_t bt = block_threads(!L.stab, L.stab ? 1u : launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride,
                                                                           L.dst, int64_t(L.n_stripes) * L.dst_stripe_stride),
-                                      L.src_stripe_stride >= 0 && L.src_stripe_stride < kWaveBlockSpan);
+                                      wave_ok);
     const Geometry g = geometry(L.len / 16, bt);
     p.units = g.units;
     p.tiles = g.tiles;

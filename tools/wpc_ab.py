@@ -56,7 +56,7 @@ def main():
                 res = {w: [] for w in WPC}
                 for _ in range(5):
                     for w in WPC:
-                        if VAR != "MEC_WPC" and w == 0:
+                        if w < 0 or (VAR != "MEC_WPC" and w == 0):  # -1: the library's default
                             os.environ.pop(VAR, None)
                         else:
                             os.environ[VAR] = str(w)
