@@ -76,9 +76,8 @@ __device__ __forceinline__ void bm_combine(const vec (&d)[W], vec (&acc)[ROWS], 
     }
 }
 
-template <int W, int R, bool G, int BT>
+template <int W, int R, bool G, int BT, int VW = bm_vw<W>()>
 __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
-    constexpr int VW = bm_vw<W>();
     constexpr int ROWS = R * W;
     typedef typename VecT<VW>::type vec;
     const uint32_t bid = block_order(p.win);
@@ -153,9 +152,9 @@ __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
 
 hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream);
 
-template <int W, int R>
-hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
-    constexpr int UB = 4 * bm_vw<W>();
+template <int W, int R, int VW>
+hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
+    constexpr int UB = 4 * VW;
     BmParams<W, R> p;
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
@@ -186,16 +185,19 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
             if (L.stab) {
                 p.s0 = s0;
-                hipLaunchKernelGGL((bm_kernel<W, R, true, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
+                if constexpr (VW == bm_vw<W>())
+                    hipLaunchKernelGGL((bm_kernel<W, R, true, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
+                else
+                    return hipErrorInvalidValue;  // gathered launches use the default lane width
             } else {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
-                const uint32_t lds = occupancy_lds(bt, std::min<uint32_t>(bt, g.units), 0, bm_target_waves(R));
+                const uint32_t lds = occupancy_lds(bt, std::min<uint32_t>(bt, g.units), 0, bm_target_waves(R, W, VW, p.win > 1));
                 if (bt == kWaveBlock)
-                    hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
+                    hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock, VW>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
                 else
-                    hipLaunchKernelGGL((bm_kernel<W, R, false, kThreads>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
+                    hipLaunchKernelGGL((bm_kernel<W, R, false, kThreads, VW>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
             }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
@@ -203,6 +205,20 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     }
     if (L.packet % UB) return launch_bm_tail(L, uint64_t(g.units) * UB, stream);
     return hipSuccess;
+}
+
+// Lane width of a strided launch (bm_lane_bytes); gathered launches keep
+// the default width.
+template <int W, int R>
+hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
+    if constexpr (bm_vw<W>() == 4) {
+        if (!L.stab) {
+            const bool in_place = launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
+                                                 int64_t(L.n_stripes) * L.dst_stripe_stride) > 1;
+            if (bm_lane_bytes(W, R, L.packet * uint64_t(L.w), in_place) == 8) return run_bm_vw<W, R, 2>(L, stream);
+        }
+    }
+    return run_bm_vw<W, R, bm_vw<W>()>(L, stream);
 }
 
 #define MEC_BM_INSTANTIATE_W(W) \

@@ -244,7 +244,20 @@ uint32_t gf8_target_waves(int k, int rows, bool in_place) {
     return in_place ? clampw(ceil_even(w), 8, 24) : clampw(ceil_even(w), 6, 20);
 }
 
-uint32_t bm_target_waves(int rows) { return clampw(uint32_t(3 * rows), 6, 16); }
+uint32_t bm_lane_bytes(int w, int rows, uint64_t chunk, bool in_place) {
+    if (w > 4) return 8;
+    const char *e = std::getenv("MEC_BM_VW");  // read per launch: experiments flip it
+    if (e) return std::atoi(e) == 2 ? 8 : 16;
+    if (!in_place) return 8;
+    return (chunk <= (8u << 10) || (rows <= 2 && chunk <= (32u << 10))) ? 8 : 16;
+}
+
+uint32_t bm_target_waves(int rows, int w, int vw, bool in_place) {
+    // w > 4 always runs 8-byte slices of twice as many packets: the
+    // 16-byte rule's bytes in flight per wave
+    if (vw >= 4 || w > 4) return clampw(uint32_t(3 * rows), 6, 16);
+    return in_place ? clampw(uint32_t(6 * rows), 6, 12) : clampw(uint32_t(6 * rows), 6, 16);
+}
 
 uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32_t waves) {
     const char *e = std::getenv("MEC_WPC");  // read per launch: experiments flip it

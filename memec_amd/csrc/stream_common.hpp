@@ -149,11 +149,31 @@ uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place = false);
 //   gf8 (all K source loads of a wave in flight at once)
 //     split outputs (encode, update):  ceil_even(64 / K + R),  6..20
 //     in place (decode):               ceil_even(64 / K + 2R), 8..24
-//   bitmatrix (one source, W packets, prefetched one ahead): 3R, 6..16
+//   bitmatrix (one source, W packets, prefetched one ahead), 16-byte
+//     slices: 3R, 6..16; 8-byte slices at w <= 4 (half the bytes in
+//     flight per wave): 6R, 6..16 split, 6..12 in place
 // in active waves (waves that own units; a block of small packets can have
 // idle ones).  MEC_WPC=<n> overrides (0 = no cap): experiments flip it.
 uint32_t gf8_target_waves(int k, int rows, bool in_place);
-uint32_t bm_target_waves(int rows);
+// Bytes per lane per packet of a strided bitmatrix launch (16 or 8; w > 4
+// always 8).  A lane of the bitmatrix kernel reads the same slice of all w
+// packets of a chunk, so a wave touches w 1 KiB address slots (mod 8 KiB)
+// per chunk where a byte-wise wave touches one.  Blocks go to the 8 XCDs
+// round-robin, and an in-place stream whose XCDs each touch one slot runs
+// at 78-80 % of 8 TB/s, 72-74 % when each XCD touches four or eight (the
+// same XOR-only kernel with its tiles rotated per stripe); the bitmatrix
+// layout of packets under 8 KiB cannot be made slot-affine, so in-place CRS
+// at 2-16 KiB chunks stays near that 72-74 % (tools/bm_variants.hip,
+// profiles/r02/xcd/).  8-byte slices halve each wave's footprint, with the
+// resident waves doubled to keep the bytes in flight (tools/bm_small_ab.py):
+//   split layouts (encode, update): 8 bytes at every chunk size, +2-4
+//     points (CRS(12,4)@64 KiB encode 80.7 -> 83.3 %);
+//   in place: 8 bytes for chunks <= 8 KiB, or <= 32 KiB with <= 2 output
+//     rows (+1-3 points; 16 bytes stay ahead above that, -5 to -9 points
+//     at 256 KiB with 8).
+// MEC_BM_VW=2|4 overrides (dwords per lane).
+uint32_t bm_lane_bytes(int w, int rows, uint64_t chunk, bool in_place);
+uint32_t bm_target_waves(int rows, int w, int vw, bool in_place);
 // Dynamic LDS bytes per block of `bt` threads (`active` of them owning
 // units, `static_lds` bytes of static LDS) so that about `waves` active waves
 // share a CU; 0 = no cap.

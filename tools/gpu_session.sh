@@ -42,7 +42,7 @@ for step in "$@"; do
         prof)
             for c in ${PROF_CONFIGS:-rs_enc}; do
                 run "prof_$c" 400 rocprofv3 --kernel-trace --stats --output-format csv \
-                    -d "$OUT/prof_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 10 --warmup 2
+                    -d "$OUT/prof_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 10
             done ;;
         pmc)
             for c in ${PROF_CONFIGS:-rs_enc}; do
