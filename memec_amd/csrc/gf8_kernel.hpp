@@ -218,12 +218,14 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     p.chunk = uint32_t(L.len);
     p.s0 = 0;
     // block size from the whole launch's layout (sub-launches share it)
-    // one-wave blocks in place only for stripe strides under kWaveBlockSpan
-    // that are not a power of two: a 512 KiB / 1 MiB stride with one-wave
-    // blocks decodes at 62-71 % of 8 TB/s, with 4-wave blocks at 77-82 %
-    // (tools/wpc_ab.py WPC_VAR=MEC_BLOCK, profiles/r02/wpc/win_pow2.log)
+    // one-wave blocks in place for stripe strides under kWaveBlockSpan,
+    // except strides of exactly 512 KiB and 1 MiB: there one-wave blocks
+    // decode at 62-71 % of 8 TB/s and 4-wave blocks at 77-82 %
+    // (tools/wpc_ab.py WPC_VAR=MEC_BLOCK, profiles/r02/wpc/win_pow2.log);
+    // other powers of two favour one-wave blocks like any stride (16 KiB:
+    // 69 -> 82 %, 2 MiB / 4 MiB +1-4; profiles/r02/gf8/rs_inplace_ab.log)
     const int64_t sss = L.src_stripe_stride;
-    const bool wave_ok = sss >= 0 && sss < kWaveBlockSpan && (sss & (sss - 1)) != 0;
+    const bool wave_ok = sss >= 0 && sss < kWaveBlockSpan && sss != (int64_t(512) << 10) && sss != (int64_t(1) << 20);
     const uint32_t bt = block_threads(!L.stab, L.stab ? 1u : launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride,
                                                                           L.dst, int64_t(L.n_stripes) * L.dst_stripe_stride),
                                       wave_ok);
@@ -251,7 +253,7 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
                 const dim3 grid(ns * g.tiles), block(bt);
-                const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, p.win > 1));
+                const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, p.win > 1, !vand));
                 if (bt == kWaveBlock) {
                     if (vand)
                         hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand, kWaveBlock>), grid, block, lds, stream, p);

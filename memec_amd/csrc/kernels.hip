@@ -239,9 +239,14 @@ uint32_t ceil_even(double x) { return 2u * uint32_t(std::ceil(x / 2.0)); }
 uint32_t clampw(uint32_t w, uint32_t lo, uint32_t hi) { return std::min(hi, std::max(lo, w)); }
 }  // namespace
 
-uint32_t gf8_target_waves(int k, int rows, bool in_place) {
+uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense) {
     const double w = 64.0 / std::max(1, k) + (in_place ? 2.0 : 1.0) * rows;
-    return in_place ? clampw(ceil_even(w), 8, 24) : clampw(ceil_even(w), 6, 20);
+    if (!in_place) return clampw(ceil_even(w), 6, 20);
+    // a dense (decode) matrix keeps each wave busy longer than the
+    // Vandermonde encode shortcut: at least 12 waves (RS(12,2) in-place
+    // decode at 128-256 KiB chunks 71 -> 76 %, RS(14,2) +1-2 points;
+    // profiles/r02/gf8/rs_inplace_ab.log, profiles/r02/wpc/wpc_pow2_strides.log)
+    return clampw(std::max(ceil_even(w), dense ? 12u : 0u), 8, 24);
 }
 
 uint32_t bm_lane_bytes(int w, int rows, uint64_t chunk, bool in_place) {
@@ -404,7 +409,7 @@ hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t
     if (len == 0) return hipSuccess;
     const uint64_t units = (len + 15) / 16, blocks = (units + kThreads - 1) / kThreads;
     // 2 source streams + 1 output per lane: the gf8 split-layout rule
-    const uint32_t lds = occupancy_lds(kThreads, kThreads, 0, gf8_target_waves(2, 1, false));
+    const uint32_t lds = occupancy_lds(kThreads, kThreads, 0, gf8_target_waves(2, 1, false, false));
     hipLaunchKernelGGL(xor_kernel, dim3(uint32_t(std::min<uint64_t>(blocks, uint64_t(1) << 22))), dim3(kThreads), lds,
                        stream, dst, a, b, len);
     return hipGetLastError();
