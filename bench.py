@@ -396,6 +396,84 @@ def host_cores():
     return threads, {"nproc": nproc, "affinity": aff, "cgroup_cpu_quota": quota}
 
 
+def probe_warmup(step, sync):
+    """Untimed warmup steps for >= 0.3 s of work (at least 3), sized from one
+    probe step after a first, cold one."""
+    step()
+    sync()
+    t0 = time.perf_counter()
+    step()
+    sync()
+    return int(min(2000, max(3, 0.3 / max(time.perf_counter() - t0, 1e-5))))
+
+
+# BASELINE configs measured beside the default line (configs[1] encode +
+# configs[2] decode), so that the driver's 1/2/4/8-GPU runs of the default
+# command record every GPU config north_star asks for: configs[3] at its
+# per-GPU batch (weak) and configs[4] encode + decode as the fixed global
+# batch of 32768 stripes sharded over the ranks (strong), as BASELINE states.
+EXTRA_CONFIGS = (("configs[3]", "rs8_small", None), ("configs[4]", "crs_enc", 32768))
+
+
+def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_ok):
+    """One BASELINE config with its own warmup, the main line's barrier +
+    max-over-ranks timing, and a verified decode: the twin decode for
+    configs[4], a decode round trip of the first stripes for configs[3]."""
+    import torch
+    from memec_amd import Codec, fill_random
+    from memec_amd.shard import shard_range, timed_steps
+
+    fam, k, m, cs, stripes, op, _ = CONFIGS[name]
+    if strong_global:
+        s0, s1 = shard_range(strong_global, rank, world)
+        stripes, global_stripes = s1 - s0, strong_global
+    else:
+        global_stripes = stripes * world
+    codec = Codec(fam, k, m, cs, device=dev.index)
+    data = torch.empty(stripes, k, cs, dtype=torch.uint8, device=dev)
+    fill_random(data, 0x4D454D4543 + 17 * (rank + 1))
+    parity = torch.empty(stripes, m, cs, dtype=torch.uint8, device=dev)
+    d = dist if world > 1 else None
+
+    def run(step, alg):
+        warm = probe_warmup(step, torch.cuda.synchronize)
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        wall, kern = timed_steps(step, steps, warm, sync=torch.cuda.synchronize, dist=d, events=ev)
+        return {"value": round(global_stripes * k * cs * steps / wall / 2**30, 3), "unit": "GiB/s",
+                "steps": steps, "warmup": warm, "ms_per_step": round(wall / steps * 1e3, 4),
+                "kernel_ms": round(kern, 4), "achieved_GBps": round(alg / (kern * 1e-3) / 1e9, 1),
+                "frac": round(alg / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+    res = {"workload": workload_name(name, stripes, bool(strong_global), global_stripes),
+           "scaling": "strong" if strong_global else "weak", "stripes_per_gpu": stripes,
+           "global_stripes": global_stripes}
+    res.update(run(lambda: codec.encode(data, parity), (k + m) * cs * stripes))
+    twin = {"crs_enc": "crs_dec"}.get(name)
+    erased = CONFIGS[twin][6] if twin else list(range(m))
+    n = stripes if twin else min(stripes, 4096)
+    st = torch.empty(n, k + m, cs, dtype=torch.uint8, device=dev)
+    st[:, :k] = data[:n]
+    st[:, k:] = parity[:n]
+    saved = st[:, erased].clone()
+    st[:, erased] = 0
+    present = sum(1 << i for i in range(k + m) if i not in erased)
+    if twin:
+        dec = run(lambda: codec.decode(st, present), (k + len(erased)) * cs * n)
+        dec["workload"] = workload_name(twin, n, True, global_stripes)
+        dec["erased"] = erased
+        dec["verified"] = all_ranks_ok(torch.equal(st[:, erased], saved))
+        res["decode"] = dec
+    else:
+        codec.decode(st, present)
+        torch.cuda.synchronize()
+        res["verified"] = all_ranks_ok(torch.equal(st[:, erased], saved))
+        res["verification"] = "decode of erasures %s restores the first %d encoded stripes" % (erased, n)
+    del data, parity, st, saved
+    codec.close()
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -409,6 +487,10 @@ def main():
     ap.add_argument("--no-secondary", action="store_true",
                     help="encode configs: skip the decode twin measurement (configs[2] for configs[1])")
     ap.add_argument("--no-ceiling", action="store_true", help="skip the on-box streaming-ceiling measurement (mec_xor)")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="default run: skip configs[3] and configs[4] beside the configs[1]/[2] line")
+    ap.add_argument("--extra-configs", action="store_true",
+                    help="measure configs[3] and configs[4] even with --stripes (multi-rank rehearsals)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory (PCIe) batch encode")
     ap.add_argument("--strong", action="store_true",
@@ -526,13 +608,7 @@ def main():
         alg_bytes = (k + len(erased)) * cs * stripes
 
     if args.warmup is None:  # size the warmup from one probe step (after a first, cold one)
-        step()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        step()
-        torch.cuda.synchronize()
-        probe = max(time.perf_counter() - t0, 1e-5)
-        args.warmup = int(min(2000, max(3, 0.3 / probe)))
+        args.warmup = probe_warmup(step, torch.cuda.synchronize)
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     wall, kern_ms = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize,
                                 dist=dist if world > 1 else None, events=ev)  # one launch per step
@@ -599,6 +675,11 @@ def main():
             os.environ["MEC_WPC"] = saved
         ceiling = 3 * a.numel() / (best * 1e-3) / 1e9
         del a, b, out
+
+    extras = None
+    if args.config == "rs_enc" and not args.strong and not args.no_extra_configs and (args.extra_configs or not args.stripes):
+        extras = {label: measure_extra(name, strong_global, args.steps, rank, world, dev, dist, all_ranks_ok)
+                  for label, name, strong_global in EXTRA_CONFIGS}
 
     ok = None
     if op == "decode" and orig is not None:
@@ -682,6 +763,8 @@ def main():
             line["dist"] = dist_info
         if e2e:
             line["e2e_host_memory"] = e2e
+        if extras:
+            line["other_configs"] = extras
         if secondary:
             line["decode"] = secondary
             if ceiling:

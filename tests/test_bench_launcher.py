@@ -70,3 +70,18 @@ def test_host_cores():
         assert threads <= max(1, int(info["cgroup_cpu_quota"] + 0.5))
     else:
         assert threads == info["affinity"]
+
+
+def test_extra_configs_are_baseline_configs():
+    """The default line's other_configs: configs[3] per GPU (weak) and
+    configs[4] as BASELINE's 32768-stripe global batch sharded over ranks."""
+    labels = {label: (name, strong) for label, name, strong in bench.EXTRA_CONFIGS}
+    assert labels == {"configs[3]": ("rs8_small", None), "configs[4]": ("crs_enc", 32768)}
+    fam, k, m, cs, stripes, op, _ = bench.CONFIGS["rs8_small"]
+    assert (fam, k, m, cs, stripes, op) == ("rs", 8, 2, 4096, 65536, "encode")
+    fam, k, m, cs, stripes, op, _ = bench.CONFIGS["crs_enc"]
+    assert (fam, k, m, cs, op) == ("cauchy", 12, 4, 65536, "encode")
+    assert bench.CONFIGS["crs_dec"][6] == [0, 1, 2, 3]
+    name = bench.workload_name("crs_enc", 4096, True, 32768)
+    assert "32768 stripes total, sharded over ranks" in name and "configs[4]" in name
+    assert bench.workload_name("rs8_small", 65536) == bench.WORKLOAD_NAMES["rs8_small"]
