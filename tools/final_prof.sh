@@ -8,4 +8,4 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_default -o run \
     -- python3 bench.py > gpurun_out/default_cmd_under_rocprof.json 2> gpurun_out/default_cmd_under_rocprof.err || exit $?
-PROF_CONFIGS="${PROF_CONFIGS:-rs_enc rs_dec crs_enc crs_dec rs8_small rs_update rs8_update}" bash tools/gpu_session.sh prof
+PROF_CONFIGS="${PROF_CONFIGS:-rs_enc rs_dec rs_dec_mixed crs_enc crs_dec rs8_small rs42 rs42_dec rs_update rs8_update}" bash tools/gpu_session.sh prof

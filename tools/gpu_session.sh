@@ -34,28 +34,28 @@ for step in "$@"; do
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py ;;
         benchall)
-            for c in rs_enc rs_dec rs_dec_mixed rs8_small crs_enc crs_dec rs42 rs42_dec; do
-                run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --steps 10
+            for c in rs_enc rs_dec rs_dec_mixed rs8_small crs_enc crs_dec rs42 rs42_dec rs_update rs8_update; do
+                run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 10
             done ;;
         batch) run bench_batch 600 python tools/bench_batch.py ;;
-        e2e) run bench_e2e 400 python bench.py --e2e --no-cpu-baseline --steps 5 ;;
+        e2e) run bench_e2e 400 python bench.py --e2e --no-cpu-baseline --no-extra-configs --steps 5 ;;
         prof)
             for c in ${PROF_CONFIGS:-rs_enc}; do
                 run "prof_$c" 400 rocprofv3 --kernel-trace --stats --output-format csv \
-                    -d "$OUT/prof_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 10
+                    -d "$OUT/prof_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 10
             done ;;
         pmc)
             for c in ${PROF_CONFIGS:-rs_enc}; do
                 run "pmc_fetch_$c" 400 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-                    -d "$OUT/pmc_fetch_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 5 --warmup 1
+                    -d "$OUT/pmc_fetch_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 5 --warmup 1
                 run "pmc_write_$c" 400 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-                    -d "$OUT/pmc_write_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 5 --warmup 1
+                    -d "$OUT/pmc_write_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 5 --warmup 1
             done ;;
         sq)
             for c in ${PROF_CONFIGS:-rs_enc}; do
                 run "pmc_sq_$c" 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU \
                     SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
-                    --output-format csv -d "$OUT/pmc_sq_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --steps 3 --warmup 1
+                    --output-format csv -d "$OUT/pmc_sq_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 3 --warmup 1
             done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
