@@ -253,7 +253,7 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
                 const dim3 grid(ns * g.tiles), block(bt);
-                const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, p.win > 1, !vand));
+                const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, p.win > 1, !vand, L.accumulate));
                 if (bt == kWaveBlock) {
                     if (vand)
                         hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand, kWaveBlock>), grid, block, lds, stream, p);

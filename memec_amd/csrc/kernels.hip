@@ -239,7 +239,12 @@ uint32_t ceil_even(double x) { return 2u * uint32_t(std::ceil(x / 2.0)); }
 uint32_t clampw(uint32_t w, uint32_t lo, uint32_t hi) { return std::min(hi, std::max(lo, w)); }
 }  // namespace
 
-uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense) {
+uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accumulate) {
+    // read-modify-write of the outputs (delta updates, K = 1): each wave
+    // also loads its R outputs; R = 2 / 3 / 4 want 16-18 / 12 / 10-12
+    // waves (tools/bm_small_ab.py update, profiles/r02/gf8/update_caps.log:
+    // RS(10,4)@1 MiB update 81.7 -> 84.1 %)
+    if (accumulate && !in_place) return clampw(ceil_even(36.0 / std::max(1, rows)), 6, 20);
     const double w = 64.0 / std::max(1, k) + (in_place ? 2.0 : 1.0) * rows;
     if (!in_place) return clampw(ceil_even(w), 6, 20);
     // a dense (decode) matrix keeps each wave busy longer than the
@@ -409,7 +414,7 @@ hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t
     if (len == 0) return hipSuccess;
     const uint64_t units = (len + 15) / 16, blocks = (units + kThreads - 1) / kThreads;
     // 2 source streams + 1 output per lane: the gf8 split-layout rule
-    const uint32_t lds = occupancy_lds(kThreads, kThreads, 0, gf8_target_waves(2, 1, false, false));
+    const uint32_t lds = occupancy_lds(kThreads, kThreads, 0, gf8_target_waves(2, 1, false, false, false));
     hipLaunchKernelGGL(xor_kernel, dim3(uint32_t(std::min<uint64_t>(blocks, uint64_t(1) << 22))), dim3(kThreads), lds,
                        stream, dst, a, b, len);
     return hipGetLastError();

@@ -147,7 +147,8 @@ uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place = false);
 // (tools/wpc_ab.py, profiles/r02/wpc/).  The right count falls as a wave's
 // own in-flight reads grow and rises with its output streams:
 //   gf8 (all K source loads of a wave in flight at once)
-//     split outputs (encode, update):  ceil_even(64 / K + R),  6..20
+//     split outputs (encode):          ceil_even(64 / K + R),  6..20
+//     read-modify-write (update):      ceil_even(36 / R),      6..20
 //     in place (decode):               ceil_even(64 / K + 2R), 8..24,
 //                                      at least 12 for dense matrices
 //   bitmatrix (one source, W packets, prefetched one ahead), 16-byte
@@ -155,7 +156,7 @@ uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place = false);
 //     flight per wave): 6R, 6..16 split, 6..12 in place
 // in active waves (waves that own units; a block of small packets can have
 // idle ones).  MEC_WPC=<n> overrides (0 = no cap): experiments flip it.
-uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense);
+uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accumulate);
 // Bytes per lane per packet of a strided bitmatrix launch (16 or 8; w > 4
 // always 8).  A lane of the bitmatrix kernel reads the same slice of all w
 // packets of a chunk, so a wave touches w 1 KiB address slots (mod 8 KiB)

@@ -6,7 +6,7 @@ and in-place decode of erasures {0..m-1}.  ~2 GiB of stripes per case, 8
 launches per sample, 5 rounds; median % of 8 TB/s.  Not product code.
 
   AB_CASES=cauchy:12:2,... AB_SIZES=8192,... AB_ARMS=-:-,64:8,256:12:2 \
-  AB_OPS=enc_split,enc_inplace,dec_inplace python3 tools/bm_small_ab.py
+  AB_OPS=enc_split,enc_inplace,dec_inplace,update python3 tools/bm_small_ab.py
 """
 import os
 import statistics
@@ -50,7 +50,13 @@ def main():
             n = max(1, int(gib * (1 << 30)) // ((k + m) * cs))
             codec = Codec(fam, k, m, cs, device=0)
             for op in OPS:
-                if op == "enc_split":
+                if op == "update":  # parity ^= A[:, j] * delta (the server's delta path)
+                    data = torch.empty(n, cs, dtype=torch.uint8, device="cuda")
+                    fill_random(data, 1)
+                    par = torch.zeros(n, m, cs, dtype=torch.uint8, device="cuda")
+                    bufs = [data, par]
+                    step = lambda: codec.encode_update(min(3, k - 1), data, par)  # noqa: E731
+                elif op == "enc_split":
                     data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
                     fill_random(data, 1)
                     par = torch.empty(n, m, cs, dtype=torch.uint8, device="cuda")
@@ -65,7 +71,7 @@ def main():
                     else:
                         present = sum(1 << i for i in range(m, k + m))
                         step = lambda: codec.decode(st, present)  # noqa: E731
-                nbytes = (k + m) * cs * n
+                nbytes = (1 + 2 * m) * cs * n if op == "update" else (k + m) * cs * n
                 res = {a: [] for a in ARMS}
                 for _ in range(5):
                     for a in ARMS:
