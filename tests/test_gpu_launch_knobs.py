@@ -1,0 +1,111 @@
+"""GPU parity under every launch shape the strided kernels can take.
+
+The launch rules (stream_common.hpp: lane width of the bitmatrix kernel,
+block size, wave caps) pick one shape per launch from the layout and the
+chunk size; the experiment knobs MEC_BM_VW / MEC_BLOCK / MEC_WPC force the
+others.  Whatever the shape, the bytes must equal the oracle's
+(Jerasure/gf_complete restatement, pinned to the reference by
+tests/golden): split and in-place encodes, in-place decodes and delta
+updates, at chunk sizes whose packets are and are not multiples of the lane
+slice (tails).
+"""
+import numpy as np
+import pytest
+
+import _oracle as O
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from memec_amd import Codec  # noqa: E402
+
+K, M, N = 6, 3, 20
+ERASED = (0, 4, 7)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    yield
+    torch.cuda.synchronize()
+
+
+def _stripes(fam, cs, seed):
+    base = O.fill(N * (K + M) * cs, seed).reshape(N, K + M, cs)
+    for s in range(N):
+        base[s, K:] = np.stack(O.encode(fam, K, M, [base[s, j].copy() for j in range(K)], cs))
+    return base
+
+
+def _check_all_layouts(fam, cs, seed):
+    base = _stripes(fam, cs, seed)
+    c = Codec(fam, K, M, cs)
+    # split encode: [s][k] data -> [s][m] parity
+    data = torch.from_numpy(np.ascontiguousarray(base[:, :K])).to("cuda")
+    par = torch.zeros(N, M, cs, dtype=torch.uint8, device="cuda")
+    c.encode(data, par)
+    torch.cuda.synchronize()
+    assert np.array_equal(par.cpu().numpy(), base[:, K:]), ("split encode", fam, cs)
+    # in-place encode: parity written inside [s][k+m]
+    st = torch.from_numpy(base.copy()).to("cuda")
+    st[:, K:] = 0
+    c.encode(st[:, :K], st[:, K:])
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), base), ("in-place encode", fam, cs)
+    # in-place decode of data and parity erasures
+    st[:, list(ERASED)] = 0
+    c.decode(st, sum(1 << i for i in range(K + M) if i not in ERASED))
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), base), ("in-place decode", fam, cs)
+    # delta update of column 2 into every parity (read-modify-write)
+    delta = O.fill(N * cs, seed + 1).reshape(N, cs)
+    par2 = torch.from_numpy(np.ascontiguousarray(base[:, K:])).to("cuda")
+    c.encode_update(2, torch.from_numpy(delta).to("cuda"), par2)
+    torch.cuda.synchronize()
+    got = par2.cpu().numpy()
+    for s in (0, N - 1):
+        d2 = base[s, :K].copy()
+        d2[2] ^= delta[s]
+        assert np.array_equal(got[s], np.stack(O.encode(fam, K, M, list(d2), cs))), ("update", fam, cs, s)
+    c.close()
+
+
+@pytest.mark.parametrize("cs", [96, 4096, 4128, 65536])
+@pytest.mark.parametrize("vw", ["2", "4", None])
+def test_bitmatrix_lane_widths(vw, cs, monkeypatch):
+    """8- and 16-byte lane slices (MEC_BM_VW), and the rule's own choice:
+    packets of 24 B and 1032 B leave tails for 16-byte slices only."""
+    if vw is None:
+        monkeypatch.delenv("MEC_BM_VW", raising=False)
+    else:
+        monkeypatch.setenv("MEC_BM_VW", vw)
+    _check_all_layouts("cauchy", cs, 900 + cs % 997)
+
+
+@pytest.mark.parametrize("fam", ["rs", "cauchy", "isal_rs"])
+@pytest.mark.parametrize("block,wpc", [("64", "0"), ("64", "6"), ("256", "24"), ("256", "0")])
+def test_block_and_wave_cap_overrides(fam, block, wpc, monkeypatch):
+    """Forced block sizes and resident-wave caps (down to one block per CU's
+    share of LDS) change timing only."""
+    monkeypatch.setenv("MEC_BLOCK", block)
+    monkeypatch.setenv("MEC_WPC", wpc)
+    _check_all_layouts(fam, 8192, 1300)
+
+
+@pytest.mark.parametrize("stride_chunk", [2048, 65536])
+def test_power_of_two_stripe_strides(stride_chunk):
+    """RS(6,2) stripes are 8 chunks: 16 KiB and 512 KiB strides, the two
+    sides of the in-place block-size rule for power-of-two strides."""
+    k, m, cs, n = 6, 2, stride_chunk, 16
+    base = O.fill(n * (k + m) * cs, 77).reshape(n, k + m, cs)
+    for s in range(n):
+        base[s, k:] = np.stack(O.encode("rs", k, m, [base[s, j].copy() for j in range(k)], cs))
+    c = Codec("rs", k, m, cs)
+    st = torch.from_numpy(base.copy()).to("cuda")
+    st[:, [0, 1]] = 0
+    c.decode(st, sum(1 << i for i in range(2, k + m)))
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), base)
+    c.close()
