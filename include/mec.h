@@ -49,7 +49,9 @@
  * Memory: the device entry points take device pointers (hipMalloc / torch
  * CUDA tensors) and a hipStream_t passed as void* (NULL = default stream);
  * they are asynchronous on that stream.  The *_host entry points take host
- * pointers and return when the result is in host memory.
+ * pointers and return when the result is in host memory.  A call with zero
+ * stripes (or zero bytes) touches no memory and succeeds; its buffer
+ * pointers may then be NULL (an empty torch tensor's data_ptr is 0).
  *
  * Layout of the batched device entry points ("strided"): chunk c of stripe s
  * starts at  base + s * stripe_stride + c * chunk_stride  (bytes).  Dense

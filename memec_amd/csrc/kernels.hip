@@ -251,7 +251,11 @@ uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accum
     // Vandermonde encode shortcut: at least 12 waves (RS(12,2) in-place
     // decode at 128-256 KiB chunks 71 -> 76 %, RS(14,2) +1-2 points;
     // profiles/r02/gf8/rs_inplace_ab.log, profiles/r02/wpc/wpc_pow2_strides.log)
-    return clampw(std::max(ceil_even(w), dense ? 12u : 0u), 8, 24);
+    if (dense) return clampw(std::max(ceil_even(w), 12u), 8, 24);
+    // the lighter Vandermonde encode in place wants the split count, 10..16
+    // (RS(10,4)@1 MiB 76.7 -> 79.5 %, RS(6,2)@256 KiB 81 -> 86 %;
+    // profiles/r02/gf8/rs104_valu_probe.log, rs_inplace_ab.log)
+    return clampw(ceil_even(64.0 / std::max(1, k) + rows), 10, 16);
 }
 
 uint32_t bm_lane_bytes(int w, int rows, uint64_t chunk, bool in_place) {

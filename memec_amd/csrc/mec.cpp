@@ -390,7 +390,7 @@ int mec_get_bitmatrix(const mec_ctx *c, int32_t *out, size_t capacity) {
 int mec_encode(mec_ctx *c, const uint8_t *data, int64_t dss_, int64_t dcs, uint8_t *parity, int64_t pss, int64_t pcs,
                uint32_t n_stripes, uint32_t parity_mask, void *stream) {
     CHECK_CTX(c);
-    if (!data || !parity) return fail(MEC_EINVAL, "null buffer");
+    if ((!data || !parity) && n_stripes) return fail(MEC_EINVAL, "null buffer");
     DeviceGuard dg(c->device);
     std::vector<uint32_t> rows = mask_rows(c, parity_mask), cols(c->k);
     for (uint32_t j = 0; j < c->k; ++j) cols[j] = j;
@@ -404,7 +404,7 @@ int mec_encode(mec_ctx *c, const uint8_t *data, int64_t dss_, int64_t dcs, uint8
 int mec_decode_split(mec_ctx *c, const uint8_t *in, int64_t iss, int64_t ics, uint8_t *out, int64_t oss, int64_t ocs,
                      uint32_t n_stripes, uint64_t present_mask, void *stream) {
     CHECK_CTX(c);
-    if (!in || !out) return fail(MEC_EINVAL, "null buffer");
+    if ((!in || !out) && n_stripes) return fail(MEC_EINVAL, "null buffer");
     std::shared_ptr<mec::LinearPlan> plan;
     int rc = get_plan(c, present_mask, plan);
     if (rc != MEC_OK) return rc;
@@ -424,7 +424,7 @@ int mec_decode(mec_ctx *c, uint8_t *chunks, int64_t ss, int64_t cs, uint32_t n_s
 int mec_encode_update(mec_ctx *c, uint32_t data_index, const uint8_t *delta, int64_t delta_ss, uint8_t *parity,
                       int64_t pss, int64_t pcs, uint32_t n_stripes, uint32_t parity_mask, void *stream) {
     CHECK_CTX(c);
-    if (!delta || !parity) return fail(MEC_EINVAL, "null buffer");
+    if ((!delta || !parity) && n_stripes) return fail(MEC_EINVAL, "null buffer");
     if (data_index >= c->k) return fail(MEC_EINVAL, "data_index %u >= k %u", data_index, c->k);
     DeviceGuard dg(c->device);
     std::vector<uint32_t> rows = mask_rows(c, parity_mask), cols{data_index};
@@ -435,13 +435,13 @@ int mec_encode_update(mec_ctx *c, uint32_t data_index, const uint8_t *delta, int
 }
 
 int mec_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, void *stream) {
-    if (!dst || !a || !b) return fail(MEC_EINVAL, "null buffer");
+    if ((!dst || !a || !b) && len) return fail(MEC_EINVAL, "null buffer");
     HIP_TRY(mec::launch_xor(dst, a, b, len, hipStream_t(stream)));
     return MEC_OK;
 }
 
 int mec_fill_random(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_offset, void *stream) {
-    if (!dst) return fail(MEC_EINVAL, "null buffer");
+    if (!dst && len) return fail(MEC_EINVAL, "null buffer");
     HIP_TRY(mec::launch_fill(dst, len, seed, word_offset, hipStream_t(stream)));
     return MEC_OK;
 }
@@ -566,7 +566,8 @@ int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta
 int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint32_t n_stripes,
                           uint32_t parity_mask) {
     CHECK_CTX(c);
-    if (!data || !parity) return fail(MEC_EINVAL, "null buffer");
+    if ((!data || !parity) && n_stripes) return fail(MEC_EINVAL, "null buffer");
+    if (!n_stripes) return MEC_OK;
     if (is_multi(c)) {
         const size_t dbytes = size_t(c->k) * c->cs, pbytes = size_t(c->m) * c->cs;
         return shard_run(c, n_stripes, [&](mec_ctx *sc, uint32_t s0, uint32_t s1) {

@@ -126,7 +126,9 @@ inline Geometry geometry(uint64_t full_units, uint32_t threads = kThreads) {
 // profiles/r01/layout/block_ab_sizes.log, block_ab_cauchy.log) find
 // in-place layouts where one-wave blocks win instead (`wave_in_place`):
 //   gf8 (byte-wise) with stripes under kWaveBlockSpan bytes: RS(4,2) /
-//     RS(10,4) in-place decode at 4 KiB-256 KiB chunks, +2-7 points;
+//     RS(10,4) in-place decode at 4 KiB-256 KiB chunks, +2-7 points —
+//     except stripe strides of exactly 512 KiB and 1 MiB, which keep
+//     4-wave blocks (run_gf8; profiles/r02/wpc/win_pow2.log);
 //   bitmatrix with chunks of kBmWaveChunk or more: CRS(12,4) / CRS(4,2)
 //     in-place decode at 256 KiB-2 MiB, +1-9 points (64 KiB keeps 4 waves:
 //     -6 points with one).
@@ -149,8 +151,8 @@ uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place = false);
 //   gf8 (all K source loads of a wave in flight at once)
 //     split outputs (encode):          ceil_even(64 / K + R),  6..20
 //     read-modify-write (update):      ceil_even(36 / R),      6..20
-//     in place (decode):               ceil_even(64 / K + 2R), 8..24,
-//                                      at least 12 for dense matrices
+//     in place, dense (decode):        ceil_even(64 / K + 2R), 12..24
+//     in place, Vandermonde (encode):  ceil_even(64 / K + R),  10..16
 //   bitmatrix (one source, W packets, prefetched one ahead), 16-byte
 //     slices: 3R, 6..16; 8-byte slices at w <= 4 (half the bytes in
 //     flight per wave): 6R, 6..16 split, 6..12 in place

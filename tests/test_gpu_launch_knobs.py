@@ -109,3 +109,30 @@ def test_power_of_two_stripe_strides(stride_chunk):
     torch.cuda.synchronize()
     assert np.array_equal(st.cpu().numpy(), base)
     c.close()
+
+
+@pytest.mark.parametrize("fam", ["rs", "cauchy", "isal_rs", "isal_cauchy"])
+def test_empty_batches_and_no_erasures(fam):
+    """Zero stripes is a successful no-op for every entry point, and a decode
+    with every chunk present returns success without writing (the
+    reference returns true for failed == 0, rscoding.cc:118-120)."""
+    k, m, cs = 4, 2, 4096
+    c = Codec(fam, k, m, cs)
+    data = torch.empty(0, k, cs, dtype=torch.uint8, device="cuda")
+    par = torch.empty(0, m, cs, dtype=torch.uint8, device="cuda")
+    c.encode(data, par)
+    c.decode(torch.empty(0, k + m, cs, dtype=torch.uint8, device="cuda"), (1 << (k + m)) - 1)
+    c.encode_update(1, torch.empty(0, cs, dtype=torch.uint8, device="cuda"), par)
+    base = _stripes_km(fam, k, m, cs, 4, 31)
+    st = torch.from_numpy(base.copy()).to("cuda")
+    c.decode(st, (1 << (k + m)) - 1)
+    torch.cuda.synchronize()
+    assert np.array_equal(st.cpu().numpy(), base)
+    c.close()
+
+
+def _stripes_km(fam, k, m, cs, n, seed):
+    base = O.fill(n * (k + m) * cs, seed).reshape(n, k + m, cs)
+    for s in range(n):
+        base[s, k:] = np.stack(O.encode(fam, k, m, [base[s, j].copy() for j in range(k)], cs))
+    return base
