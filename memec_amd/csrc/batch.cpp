@@ -276,8 +276,18 @@ struct SlotHold {
 
 // stab / dtab: host arrays of n rows of device chunk pointers; pat: per-stripe
 // map index (nullptr = map 0).
+// 1 if the chunk pointers of the first stripes (a sample: the shape only
+// steers the launch, never the result) are all 16-byte aligned, else 2.
+uint8_t gather_shape(const void *tab, uint32_t stride, uint32_t n) {
+    const uint64_t *t = static_cast<const uint64_t *>(tab);
+    uint64_t bits = 0;
+    const size_t cnt = size_t(std::min<uint32_t>(n, 64)) * stride;
+    for (size_t i = 0; i < cnt; ++i) bits |= t[i];
+    return (bits & 15) ? 2 : 1;
+}
+
 int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, const void *dtab, uint32_t dstride,
-               const uint16_t *pat, uint32_t n, hipStream_t st, bool mapped_tables = false) {
+               const uint16_t *pat, uint32_t n, hipStream_t st, bool mapped_tables = false, bool device_mem = true) {
     if (M.ssel.empty() || M.rows() == 0 || n == 0) return MEC_OK;
     // a single map with no skipped stripe runs from kernel arguments;
     // anything else through per-stripe descriptors
@@ -320,6 +330,7 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
                 L.len = c->cs;
                 L.n_stripes = n;
                 L.accumulate = M.accumulate;
+                L.gshape = device_mem ? std::max(gather_shape(stab, sstride, n), gather_shape(dtab, dstride, n)) : 0;
                 for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
                 for (int i = 0; i < nr; ++i) {
                     L.dst_off[i] = ds[r0 + i];
@@ -473,7 +484,7 @@ int run_zerocopy(mec_ctx *c, std::vector<Group> &gs) {
         M.add(ss, ds, g.coef);
         // small batches (coalesced single-stripe calls) read their pointer
         // rows in place from pinned memory: one launch, no table copy
-        rc = run_gather(c, M, rows[q].data(), row, rows[q].data(), row, nullptr, g.n, h.l->stream, g.n <= 256);
+        rc = run_gather(c, M, rows[q].data(), row, rows[q].data(), row, nullptr, g.n, h.l->stream, g.n <= 256, false);
     }
     // no launch may outlive the call (the caller owns the chunks)
     hipError_t e = lane_sync(h.l->stream);

@@ -226,9 +226,10 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     // 69 -> 82 %, 2 MiB / 4 MiB +1-4; profiles/r02/gf8/rs_inplace_ab.log)
     const int64_t sss = L.src_stripe_stride;
     const bool wave_ok = sss >= 0 && sss < kWaveBlockSpan && sss != (int64_t(512) << 10) && sss != (int64_t(1) << 20);
-    const uint32_t bt = block_threads(!L.stab, L.stab ? 1u : launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride,
-                                                                          L.dst, int64_t(L.n_stripes) * L.dst_stripe_stride),
-                                      wave_ok);
+    const uint32_t bt = L.stab ? gathered_block_threads(L.gshape)
+                               : block_threads(true, launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
+                                                                    int64_t(L.n_stripes) * L.dst_stripe_stride),
+                                               wave_ok);
     const Geometry g = geometry(L.len / 16, bt);
     p.units = g.units;
     p.tiles = g.tiles;
@@ -244,10 +245,19 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
             if (L.stab) {
                 p.s0 = s0;
-                if (vand)
-                    hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Vand, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
-                else
-                    hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Dense, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
+                const dim3 grid(ns * g.tiles), block(bt);
+                const uint32_t lds = gathered_lds(bt, R * K * 32, L.gshape);
+                if (bt == kWaveBlock) {
+                    if (vand)
+                        hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Vand, kWaveBlock>), grid, block, lds, stream, p);
+                    else
+                        hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Dense, kWaveBlock>), grid, block, lds, stream, p);
+                } else {
+                    if (vand)
+                        hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Vand, kThreads>), grid, block, lds, stream, p);
+                    else
+                        hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Dense, kThreads>), grid, block, lds, stream, p);
+                }
             } else {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;

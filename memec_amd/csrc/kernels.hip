@@ -234,6 +234,22 @@ uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place) {
     if (win == 1) return uint32_t(kWaveBlock);
     return wave_in_place ? uint32_t(kWaveBlock) : uint32_t(kThreads);
 }
+uint32_t gathered_block_threads(uint8_t gshape) {
+    const char *e = std::getenv("MEC_GBLOCK");  // read per launch: experiments flip it
+    if (e) return std::atoi(e) == kWaveBlock ? uint32_t(kWaveBlock) : uint32_t(kThreads);
+    return gshape == 1 ? uint32_t(kWaveBlock) : uint32_t(kThreads);
+}
+uint32_t gathered_lds(uint32_t bt, uint32_t static_lds, uint8_t gshape) {
+    const char *e = std::getenv("MEC_GWPC");
+    const int w = e ? std::atoi(e) : (gshape == 1 ? 16 : gshape == 2 ? 12 : 0);
+    if (w <= 0) return 0;
+    constexpr uint32_t kLdsPerCu = 160u << 10, kGranule = 512;
+    const uint32_t per = std::max<uint32_t>(1, bt / 64);
+    const uint32_t blocks = std::max<uint32_t>(1, (uint32_t(w) + per - 1) / per);
+    const uint32_t per_block = kLdsPerCu / blocks / kGranule * kGranule;
+    const uint32_t used = (static_lds + kGranule - 1) / kGranule * kGranule;
+    return per_block > used + kGranule ? per_block - used - kGranule : 0;
+}
 namespace {
 uint32_t ceil_even(double x) { return 2u * uint32_t(std::ceil(x / 2.0)); }
 uint32_t clampw(uint32_t w, uint32_t lo, uint32_t hi) { return std::min(hi, std::max(lo, w)); }

@@ -37,6 +37,10 @@ struct Gf8Launch {
     uint64_t len;          // bytes per chunk region
     uint32_t n_stripes;
     bool accumulate;       // XOR into dst instead of overwriting
+    // pointer tables over device memory: 1 = every sampled chunk 16-byte
+    // aligned, 2 = some are not (MemEC's 8-byte ChunkPool headers); 0 =
+    // unknown / host memory (gathered_block_threads)
+    uint8_t gshape;
     Gf8Coef coef[kMaxRows][kMaxSrc];
 };
 
