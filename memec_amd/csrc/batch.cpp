@@ -350,6 +350,7 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
                 L.packet = c->packet;
                 L.n_stripes = n;
                 L.accumulate = M.accumulate;
+                L.gshape = device_mem ? std::max(gather_shape(stab, sstride, n), gather_shape(dtab, dstride, n)) : 0;
                 for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
                 for (int i = 0; i < nr; ++i) {
                     L.dst_off[i] = ds[r0 + i];

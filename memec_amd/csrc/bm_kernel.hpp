@@ -167,9 +167,14 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
     p.chunk = uint32_t(L.packet * uint64_t(L.w));
     p.s0 = 0;
     // block size from the whole launch's layout (sub-launches share it)
-    const uint32_t bt = block_threads(!L.stab, L.stab ? 1u : launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride,
-                                                                          L.dst, int64_t(L.n_stripes) * L.dst_stripe_stride),
-                                      uint64_t(p.chunk) >= kBmWaveChunk);
+    // gathered: aligned chunks keep the default shape (one-wave blocks cost
+    // the bitmatrix kernel 3.5 % on aligned decode batches), unaligned ones
+    // take the capped 4-wave shape (+1-3 %; profiles/r02/host/gather_ab_bm.log)
+    const uint8_t gshape = L.gshape == 1 ? 0 : L.gshape;
+    const uint32_t bt = L.stab ? gathered_block_threads(gshape)
+                               : block_threads(true, launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
+                                                                    int64_t(L.n_stripes) * L.dst_stripe_stride),
+                                               uint64_t(p.chunk) >= kBmWaveChunk);
     const Geometry g = geometry(L.packet / UB, bt);
     p.units = g.units;
     p.tiles = g.tiles;
@@ -185,10 +190,15 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
             if (L.stab) {
                 p.s0 = s0;
-                if constexpr (VW == bm_vw<W>())
-                    hipLaunchKernelGGL((bm_kernel<W, R, true, kThreads>), dim3(ns * g.tiles), dim3(bt), 0, stream, p);
-                else
+                if constexpr (VW == bm_vw<W>()) {
+                    const uint32_t glds = gathered_lds(bt, 0, gshape);
+                    if (bt == kWaveBlock)
+                        hipLaunchKernelGGL((bm_kernel<W, R, true, kWaveBlock>), dim3(ns * g.tiles), dim3(bt), glds, stream, p);
+                    else
+                        hipLaunchKernelGGL((bm_kernel<W, R, true, kThreads>), dim3(ns * g.tiles), dim3(bt), glds, stream, p);
+                } else {
                     return hipErrorInvalidValue;  // gathered launches use the default lane width
+                }
             } else {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;

@@ -59,6 +59,7 @@ struct BmLaunch {
     uint64_t packet;
     uint32_t n_stripes;
     bool accumulate;
+    uint8_t gshape;        // as Gf8Launch::gshape
     uint8_t mask[kMaxSrc][kMaxBmRows];
 };
 
