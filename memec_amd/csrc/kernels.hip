@@ -239,16 +239,23 @@ uint32_t gathered_block_threads(uint8_t gshape) {
     if (e) return std::atoi(e) == kWaveBlock ? uint32_t(kWaveBlock) : uint32_t(kThreads);
     return gshape == 1 ? uint32_t(kWaveBlock) : uint32_t(kThreads);
 }
-uint32_t gathered_lds(uint32_t bt, uint32_t static_lds, uint8_t gshape) {
-    const char *e = std::getenv("MEC_GWPC");
-    const int w = e ? std::atoi(e) : (gshape == 1 ? 16 : gshape == 2 ? 12 : 0);
-    if (w <= 0) return 0;
+namespace {
+// Dynamic LDS per block so that about `waves` active waves share a CU (each
+// block has `per` active waves); 0 when no LDS is left to reserve.
+uint32_t lds_for_waves(uint32_t per, uint32_t static_lds, uint32_t waves) {
     constexpr uint32_t kLdsPerCu = 160u << 10, kGranule = 512;
-    const uint32_t per = std::max<uint32_t>(1, bt / 64);
-    const uint32_t blocks = std::max<uint32_t>(1, (uint32_t(w) + per - 1) / per);
+    const uint32_t blocks = std::max<uint32_t>(1, (waves + per - 1) / per);
     const uint32_t per_block = kLdsPerCu / blocks / kGranule * kGranule;
     const uint32_t used = (static_lds + kGranule - 1) / kGranule * kGranule;
     return per_block > used + kGranule ? per_block - used - kGranule : 0;
+}
+}  // namespace
+
+uint32_t gathered_lds(uint32_t bt, uint32_t static_lds, uint8_t gshape) {
+    const char *e = std::getenv("MEC_GWPC");  // read per launch: experiments flip it
+    const int w = e ? std::atoi(e) : (gshape == 1 ? 16 : gshape == 2 ? 12 : 0);
+    if (w <= 0) return 0;
+    return lds_for_waves(std::max<uint32_t>(1, bt / 64), static_lds, uint32_t(w));
 }
 namespace {
 uint32_t ceil_even(double x) { return 2u * uint32_t(std::ceil(x / 2.0)); }
@@ -296,13 +303,8 @@ uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32
     // per wave for a cap to pay (CRS at 2 KiB chunks: 75 % uncapped, 51 %
     // capped, profiles/r02/sweep)
     if (waves == 0 || (!e && active < 64)) return 0;
-    constexpr uint32_t kLdsPerCu = 160u << 10, kGranule = 512;
-    const uint32_t per = std::max<uint32_t>(1, std::min(bt, std::max<uint32_t>(active, 1)) / 64 +
-                                                   (std::min(bt, std::max<uint32_t>(active, 1)) % 64 ? 1 : 0));
-    const uint32_t blocks = std::max<uint32_t>(1, (waves + per - 1) / per);
-    const uint32_t per_block = kLdsPerCu / blocks / kGranule * kGranule;
-    const uint32_t used = (static_lds + kGranule - 1) / kGranule * kGranule;
-    return per_block > used + kGranule ? per_block - used - kGranule : 0;
+    const uint32_t act = std::min(bt, std::max<uint32_t>(active, 1));
+    return lds_for_waves(std::max<uint32_t>(1, (act + 63) / 64), static_lds, waves);
 }
 }  // namespace detail
 
