@@ -18,7 +18,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 from cap_ab import workload  # noqa: E402
 
-KNOBS = ("MEC_BLOCK", "MEC_WINDOWS", "MEC_WPC", "MEC_BM_VW", "MEC_XCD_ORDER")
+KNOBS = ("MEC_BLOCK", "MEC_WINDOWS", "MEC_WPC", "MEC_BM_VW", "MEC_ONES")
 
 
 def parse_arms(text):
