@@ -16,7 +16,7 @@ idles out and is relaunched by the next callers many times a second.
 Every call's bytes are checked; one JSON line per (family, shape).
 Not product code.
 
-  SOAK_SECONDS=60 SOAK_THREADS=16 python3 tools/queue_soak.py
+  SOAK_SECONDS=60 SOAK_THREADS=16 [SOAK_STAGED=1] python3 tools/queue_soak.py
 """
 import json
 import os
@@ -44,6 +44,9 @@ SHAPES = [("rs", 8, 2, 4096), ("cauchy", 12, 4, 4096), ("rs", 10, 4, 16384), ("c
 def soak(fam, k, m, cs, threads, seconds, slots):
     n = k + m + 1  # + one delta slot per stripe
     slab = Slab(threads * n, cs, 7 + k)
+    staged = os.environ.get("SOAK_STAGED") == "1"
+    if staged:  # unregistered chunks: calls are staged through mapped pinned lanes
+        slab.close()
     c = Codec(fam, k, m, cs)
     c.set_host_queue(slots)
     wants, origs = [], []
@@ -106,8 +109,9 @@ def soak(fam, k, m, cs, threads, seconds, slots):
     dt = time.time() - t0
     st = c.stats()
     c.close()
-    slab.close()
-    return {"family": fam, "k": k, "m": m, "chunk": cs, "threads": threads, "slots": slots,
+    if not staged:
+        slab.close()
+    return {"family": fam, "k": k, "m": m, "chunk": cs, "threads": threads, "slots": slots, "staged": staged,
             "seconds": round(dt, 1), "calls": sum(counts), "calls_per_s": round(sum(counts) / dt),
             "queue_calls": st["queue_calls"] - st0["queue_calls"],
             "queue_launches": st["queue_launches"] - st0["queue_launches"],
