@@ -277,13 +277,16 @@ struct SlotHold {
 // stab / dtab: host arrays of n rows of device chunk pointers; pat: per-stripe
 // map index (nullptr = map 0).
 // 1 if the chunk pointers of the first stripes (a sample: the shape only
-// steers the launch, never the result) are all 16-byte aligned, else 2.
+// steers the launch, never the result) are all 128-byte (cache-line)
+// aligned, else 2.  16-byte alignment is not enough: chunks at 16 or 64 mod
+// 128 run 6-14 % faster with the 4-wave shape (tools/gather_ab.py,
+// profiles/r02/host/gather_ab_hdr.log; tools/align_probe.hip).
 uint8_t gather_shape(const void *tab, uint32_t stride, uint32_t n) {
     const uint64_t *t = static_cast<const uint64_t *>(tab);
     uint64_t bits = 0;
     const size_t cnt = size_t(std::min<uint32_t>(n, 64)) * stride;
     for (size_t i = 0; i < cnt; ++i) bits |= t[i];
-    return (bits & 15) ? 2 : 1;
+    return (bits & 127) ? 2 : 1;
 }
 
 int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, const void *dtab, uint32_t dstride,

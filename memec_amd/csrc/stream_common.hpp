@@ -141,9 +141,9 @@ constexpr int64_t kWaveBlockSpan = int64_t(8) << 20;
 constexpr uint64_t kBmWaveChunk = uint64_t(256) << 10;
 uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place = false);
 // Single-map gathered gf8 launches (pointer tables) over device memory:
-// 16-byte-aligned chunks take one-wave blocks with 16 resident waves per
-// CU, unaligned ones (8-byte ChunkPool headers: each wave's 1 KiB straddles
-// an extra line) 4-wave blocks with 12; host memory and unknown layouts keep
+// line-aligned (128-byte) chunks take one-wave blocks with 16 resident waves
+// per CU, others (8-byte ChunkPool headers, or 16-byte-aligned slots off the
+// line grid: each wave's 1 KiB straddles an extra line) 4-wave blocks with 12; host memory and unknown layouts keep
 // 4-wave blocks, uncapped (tools/gather_ab.py, profiles/r02/host/
 // gather_ab2.log: +2-6 % aligned, +3-7 % unaligned at 64 KiB-1 MiB).
 // Experiment knobs MEC_GBLOCK=64|256 and MEC_GWPC=<waves> (0 = no cap).

@@ -28,7 +28,10 @@ CASES = [("rs", 10, 4, 1 << 20, 1024, 8, "encode"), ("rs", 10, 4, 1 << 20, 1024,
          ("rs", 10, 4, 1 << 20, 1024, 8, "decode"), ("rs", 10, 4, 1 << 20, 1024, 256, "decode"),
          ("rs", 10, 4, 65536, 4096, -1, "decode"), ("rs", 10, 4, 65536, 4096, 8, "decode"),
          ("cauchy", 12, 4, 65536, 4096, 8, "encode"), ("cauchy", 12, 4, 65536, 4096, 256, "encode"),
-         ("cauchy", 12, 4, 65536, 4096, -1, "decode"), ("cauchy", 12, 4, 65536, 4096, 8, "decode")]
+         ("cauchy", 12, 4, 65536, 4096, -1, "decode"), ("cauchy", 12, 4, 65536, 4096, 8, "decode"),
+         # 13..: 16-byte-aligned slots that are not line-aligned (tools/align_probe.hip)
+         ("rs", 10, 4, 1 << 20, 1024, 16, "encode"), ("rs", 10, 4, 65536, 4096, 16, "encode"),
+         ("rs", 10, 4, 65536, 4096, 64, "decode"), ("rs", 10, 4, 1 << 20, 1024, 128, "encode")]
 if os.environ.get("GA_CASES"):  # indices into CASES
     CASES = [CASES[int(i)] for i in os.environ["GA_CASES"].split(",")]
 
