@@ -433,7 +433,7 @@ def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_
     data = torch.empty(stripes, k, cs, dtype=torch.uint8, device=dev)
     fill_random(data, 0x4D454D4543 + 17 * (rank + 1))
     parity = torch.empty(stripes, m, cs, dtype=torch.uint8, device=dev)
-    d = dist if world > 1 else None
+    d = dist if dist.is_initialized() else None
 
     def run(step, alg):
         warm = probe_warmup(step, torch.cuda.synchronize)
@@ -536,7 +536,12 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist_info = None
-    if world > 1:
+    # a process group whenever a launcher started the job, one rank included
+    # (`torchrun --nproc-per-node 1 bench.py` runs the RCCL init, barriers
+    # and max-over-ranks reductions on a one-GPU box); `python bench.py`
+    # alone is the plain N=1 run
+    use_pg = world > 1 or "WORLD_SIZE" in os.environ
+    if use_pg:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -551,7 +556,7 @@ def main():
 
     def all_ranks_ok(flag):
         """A verification holds only if it held on every rank."""
-        if world == 1:
+        if not use_pg:
             return bool(flag)
         bad = max_over_ranks([0.0 if flag else 1.0], dist,
                              device="cpu" if dist.get_backend() == "gloo" else dev)
@@ -611,7 +616,7 @@ def main():
         args.warmup = probe_warmup(step, torch.cuda.synchronize)
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     wall, kern_ms = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize,
-                                dist=dist if world > 1 else None, events=ev)  # one launch per step
+                                dist=dist if use_pg else None, events=ev)  # one launch per step
 
     # the metric is encode+decode: an encode config also times its decode
     # twin (configs[2] for configs[1]) on the just-encoded stripes, every
@@ -631,7 +636,7 @@ def main():
         dpresent = sum(1 << i for i in range(k + m) if i not in derased)
         dev_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
         dwall, dkern = timed_steps(lambda: codec.decode(st, dpresent), args.steps, args.warmup,
-                                   sync=torch.cuda.synchronize, dist=dist if world > 1 else None, events=dev_ev)
+                                   sync=torch.cuda.synchronize, dist=dist if use_pg else None, events=dev_ev)
         dalg = (k + len(derased)) * cs * stripes
         secondary = {"workload": workload_name(twin, stripes, args.strong, global_stripes), "erased": derased,
                      "value": round(global_stripes * k * cs * args.steps / dwall / 2**30, 3), "unit": "GiB/s",
@@ -800,7 +805,7 @@ def main():
                 if cb and "error" not in cb:
                     cb["host"] = dict(host, threads_used=threads)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -24,7 +24,7 @@ def dist_env():
 
 def max_over_ranks(values, dist=None, device="cpu"):
     """Element-wise max of a list of floats over all ranks."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if dist is None or not dist.is_initialized():
         return list(values)
     import torch
     t = torch.tensor(list(values), dtype=torch.float64, device=device)
@@ -40,7 +40,7 @@ def timed_steps(step, steps, warmup, sync=None, dist=None, events=None):
     events: optional (start_event, end_event) recorded on the launch stream
     around the timed steps (device-side duration)."""
     sync = sync or (lambda: None)
-    use_dist = dist is not None and dist.is_initialized() and dist.get_world_size() > 1
+    use_dist = dist is not None and dist.is_initialized()
     for _ in range(warmup):
         step()
     sync()

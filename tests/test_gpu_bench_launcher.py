@@ -42,3 +42,28 @@ def test_bench_gpus2_strong_crs():
     assert rec["n_gpus"] == 2 and rec["scaling"] == "strong"
     assert rec["config"]["global_stripes"] == 96 and rec["config"]["stripes_per_gpu"] == 48
     assert rec["decode"]["verified"] is True
+
+
+def test_bench_under_launcher_uses_rccl():
+    """Under torch.distributed.run, one rank on the one-GPU box: the same
+    RCCL ("nccl") process group, barriers and max-over-ranks reductions the
+    driver's 2/4/8-GPU runs use, exercised on the hardware."""
+    env = dict(os.environ)
+    env.pop("MEC_BENCH_DIST_BACKEND", None)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(v, None)
+    sys.path.insert(0, ROOT)
+    import bench
+    cmd = bench.launcher_cmd(["--gpus", "1", "--steps", "3", "--warmup", "1", "--no-ceiling", "--no-cpu-baseline",
+                              "--stripes", "64", "--extra-configs"], 1, bench._free_port())
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 1
+    assert rec["dist"]["backend"] == "nccl" and rec["dist"]["rccl"] is True and rec["dist"]["world_size"] == 1
+    assert rec["decode"]["verified"] is True
+    assert rec["other_configs"]["configs[3]"]["verified"] is True
+    assert rec["other_configs"]["configs[4]"]["decode"]["verified"] is True
