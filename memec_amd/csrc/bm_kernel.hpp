@@ -49,6 +49,7 @@ struct BmParams {
     uint32_t sstride, dstride, chunk, s0;
     uint64_t packet;
     uint32_t units, tiles, k, accumulate, win, pad;
+    uint32_t nstr, sgroup, srun, pad2;  // stripe-group map (stream_common.hpp stripe_tile)
     int64_t src_off[kMaxSrc];
     int64_t dst_off[R];
     uint8_t mask[kMaxSrc][R * W];
@@ -81,8 +82,9 @@ __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
     constexpr int ROWS = R * W;
     typedef typename VecT<VW>::type vec;
     const uint32_t bid = block_order(p.win);
-    const uint32_t stripe = bid / p.tiles;
-    const uint32_t u = (bid - stripe * p.tiles) * BT + threadIdx.x;
+    uint32_t stripe, tile;
+    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, stripe, tile);
+    const uint32_t u = tile * BT + threadIdx.x;
     if (u >= p.units) return;
     vec acc[ROWS];
     vec d[W], nx[W];
@@ -181,6 +183,10 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
     p.accumulate = L.accumulate ? 1u : 0u;
     p.win = 1;
     p.pad = 0;
+    p.nstr = 0;
+    p.sgroup = 0;
+    p.srun = 8;
+    p.pad2 = 0;
     for (int j = 0; j < kMaxSrc; ++j) p.src_off[j] = j < L.k ? L.src_off[j] : 0;
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int j = 0; j < kMaxSrc; ++j)
@@ -203,6 +209,8 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
+                p.nstr = ns;
+                p.sgroup = stripe_group(p.chunk, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, true, p.srun);
                 const uint32_t lds = occupancy_lds(bt, std::min<uint32_t>(bt, g.units), 0, bm_target_waves(R, W, VW, p.win > 1));
                 if (bt == kWaveBlock)
                     hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock, VW>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);

@@ -31,6 +31,7 @@ struct Gf8Params {
     const uint64_t *stab, *dtab;
     uint32_t sstride, dstride, chunk, s0;
     uint32_t units, tiles, accumulate, win;
+    uint32_t nstr, sgroup, srun;  // stripes in this launch, stripe group and run (stripe_tile)
     int64_t src_off[K];
     int64_t dst_off[R];
     Gf8Coef coef[R][K];
@@ -149,8 +150,9 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     }
     __syncthreads();
     const uint32_t bid = block_order(p.win);
-    const uint32_t stripe = bid / p.tiles;
-    const uint32_t u = (bid - stripe * p.tiles) * BT + threadIdx.x;
+    uint32_t stripe, tile;
+    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, stripe, tile);
+    const uint32_t u = tile * BT + threadIdx.x;
     if (u >= p.units) return;
     u32x4 d[K];
     u32x4 acc[R];
@@ -235,6 +237,9 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     p.tiles = g.tiles;
     p.accumulate = L.accumulate ? 1u : 0u;
     p.win = 1;
+    p.nstr = 0;
+    p.sgroup = 0;
+    p.srun = 8;
     for (int j = 0; j < K; ++j) p.src_off[j] = L.src_off[j];
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int i = 0; i < R; ++i)
@@ -262,6 +267,8 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
+                p.nstr = ns;
+                p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
                 const dim3 grid(ns * g.tiles), block(bt);
                 const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, p.win > 1, !vand, L.accumulate));
                 if (bt == kWaveBlock) {

@@ -21,6 +21,7 @@
 #include <array>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <utility>
 
 #include "gf_math.hpp"
@@ -217,6 +218,28 @@ hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream) {
 using namespace detail;
 
 namespace detail {
+uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool in_place, bool bitmatrix,
+                      uint32_t &run) {
+    const char *e = std::getenv("MEC_SGROUP");  // read per launch: experiments flip it
+    run = 8;
+    // chunks of 2 MiB or more: 16 stripes, runs of 8 tiles
+    // (tools/sgroup_ab.py, profiles/r02/sgroup/; RS(10,4) split encode 2 MiB
+    // 75.7 -> 78.8-80.0 %, 4 MiB 72.4 -> 77.2, 8 MiB 67.1 -> 79.2, 16 MiB
+    // 57.4 -> 80.1; in-place decode 2 MiB 76.6 -> 78.5, 4 MiB 57.5 -> 76.0,
+    // 8 MiB 59.0 -> 78.1); at 256 KiB-1 MiB every group costs 1-10 points.
+    // Not for the bitmatrix kernel, whose lanes already read w packets a
+    // packet apart: CRS(12,4) 2 MiB encode 76.4 -> 72.8 %, decode 72.2 ->
+    // 68.7 with the same map (profiles/r02/sgroup/sgroup_ab_crs.log)
+    (void)in_place;
+    uint32_t g = (!bitmatrix && chunk >= (uint64_t(2) << 20)) ? 16u : 0u;
+    if (e) {
+        g = uint32_t(std::atoi(e));
+        if (const char *c = std::strchr(e, ':')) run = uint32_t(std::atoi(c + 1));
+    }
+    if (g <= 1 || run == 0 || run % 8 != 0 || tiles % run != 0 || n_stripes < 2) return 0;
+    return std::min(g, n_stripes);
+}
+
 uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span) {
     const char *e = std::getenv("MEC_WINDOWS");  // read per launch: experiments flip it
     const int forced = e ? std::atoi(e) : 0;

@@ -79,6 +79,39 @@ __device__ __forceinline__ uint32_t block_order(uint32_t win) {
     return b < per * win ? (b % win) * per + b / win : b;
 }
 
+// Stripe groups.  With the identity map the resident blocks of a launch
+// cover a few thousand consecutive tiles, i.e. only the first one to three
+// stripes of 1 MiB chunks and less than one stripe of larger ones, every
+// wave reading its k chunks at the same offset, chunk-size bytes apart;
+// RS(10,4) encode runs 84 % of 8 TB/s at 64 KiB chunks, 81 % at 1 MiB, 72 %
+// at 4 MiB and 57 % at 16 MiB for the same bytes (tools/stride_probe.py,
+// tools/sgroup_ab.py).  A group map
+// walks `group` stripes at a time: consecutive blocks take 8 consecutive
+// tiles (so block id mod 8, the XCD, still fixes the tile mod 8, as in the
+// identity map), then the next stripe of the group, and only after every
+// stripe of the group the next 8 tiles.  group = 0 keeps the identity map;
+// tiles % run == 0 and run % 8 == 0 whenever group != 0 (host side,
+// stripe_group; `run` consecutive tiles per stripe visit, default 8).
+__device__ __forceinline__ void stripe_tile(uint32_t bid, uint32_t tiles, uint32_t ns, uint32_t group, uint32_t run,
+                                            uint32_t &stripe, uint32_t &tile) {
+    if (group == 0) {
+        stripe = bid / tiles;
+        tile = bid - stripe * tiles;
+        return;
+    }
+    const uint32_t per = group * tiles;
+    const uint32_t g = bid / per, r = bid - g * per;
+    const uint32_t gl = ns - g * group < group ? ns - g * group : group;
+    const uint32_t q = r / run, sl = q % gl;
+    stripe = g * group + sl;
+    tile = (q / gl) * run + (r - q * run);
+}
+// Host: stripes per group for a strided launch of `tiles` blocks per stripe
+// (0 = identity) and the run length.  MEC_SGROUP=<n>[:<run>] overrides
+// (experiments flip it).
+uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool in_place, bool bitmatrix,
+                      uint32_t &run);
+
 // Host: windows for a strided launch — 2 when the output region lies inside
 // the input region's stripe span (one allocation, interleaved), else 1.
 // MEC_WINDOWS=<n> overrides (layout experiments).

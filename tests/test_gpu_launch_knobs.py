@@ -136,3 +136,38 @@ def _stripes_km(fam, k, m, cs, n, seed):
     for s in range(n):
         base[s, k:] = np.stack(O.encode(fam, k, m, [base[s, j].copy() for j in range(k)], cs))
     return base
+
+
+@pytest.mark.parametrize("group", ["0", "3:8", "7:16", "4:64", "64:8", "bad:7"])
+def test_stripe_group_overrides(group, monkeypatch):
+    """The stripe-group block map (stream_common.hpp stripe_tile) with
+    forced groups and run lengths, a last group shorter than the rest
+    (N = 20 stripes), and an invalid run (falls back to the identity map):
+    every layout stays bit-exact.  64 KiB chunks: 64 one-wave tiles."""
+    monkeypatch.setenv("MEC_SGROUP", group)
+    _check_all_layouts("rs", 65536, 1500)
+
+
+def test_stripe_groups_default_rule_large_chunks(monkeypatch):
+    """Split-layout encodes with chunks of 2 MiB or more take the grouped
+    map by default (16 stripes, runs of 8 tiles): RS(4,2) at 2 MiB over 19
+    stripes (one full group and a short one) equals the identity map, and
+    its first and last stripes equal the oracle."""
+    k, m, cs, n = 4, 2, 2 << 20, 19
+    monkeypatch.delenv("MEC_SGROUP", raising=False)
+    c = Codec("rs", k, m, cs)
+    data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
+    from memec_amd import fill_random
+    fill_random(data, 4242)
+    par = torch.zeros(n, m, cs, dtype=torch.uint8, device="cuda")
+    c.encode(data, par)
+    monkeypatch.setenv("MEC_SGROUP", "0")
+    ref = torch.zeros_like(par)
+    c.encode(data, ref)
+    torch.cuda.synchronize()
+    assert torch.equal(par, ref)
+    host = data.cpu().numpy()
+    got = par.cpu().numpy()
+    for s in (0, n - 1):
+        assert np.array_equal(got[s], np.stack(O.encode("rs", k, m, [host[s, j].copy() for j in range(k)], cs)))
+    c.close()
