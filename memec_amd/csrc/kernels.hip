@@ -233,6 +233,7 @@ uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool i
     (void)in_place;
     uint32_t g = (!bitmatrix && chunk >= (uint64_t(2) << 20)) ? 16u : 0u;
     if (e) {
+        if (e[0] == 'x') return tiles % 8 == 0 ? kXcdRegions : 0u;
         g = uint32_t(std::atoi(e));
         if (const char *c = std::strchr(e, ':')) run = uint32_t(std::atoi(c + 1));
     }

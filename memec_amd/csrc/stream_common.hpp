@@ -92,11 +92,18 @@ __device__ __forceinline__ uint32_t block_order(uint32_t win) {
 // stripe of the group the next 8 tiles.  group = 0 keeps the identity map;
 // tiles % run == 0 and run % 8 == 0 whenever group != 0 (host side,
 // stripe_group; `run` consecutive tiles per stripe visit, default 8).
+constexpr uint32_t kXcdRegions = 0xffffffffu;  // stripe_group value of MEC_SGROUP=x
 __device__ __forceinline__ void stripe_tile(uint32_t bid, uint32_t tiles, uint32_t ns, uint32_t group, uint32_t run,
                                             uint32_t &stripe, uint32_t &tile) {
     if (group == 0) {
         stripe = bid / tiles;
         tile = bid - stripe * tiles;
+        return;
+    }
+    if (group == kXcdRegions) {  // experiment: XCD x (block id mod 8) takes the x-th eighth of each stripe
+        stripe = bid / tiles;
+        const uint32_t r = bid - stripe * tiles;
+        tile = (r & 7) * (tiles >> 3) + (r >> 3);
         return;
     }
     const uint32_t per = group * tiles;
