@@ -617,16 +617,25 @@ int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint
     std::vector<int64_t> so(c->k), dof(rows.size());
     for (uint32_t j = 0; j < c->k; ++j) so[j] = int64_t(j) * int64_t(cs);
     for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(rows[r]) * int64_t(cs);
+    // on any failure both streams are drained before returning, so no copy
+    // queued here still writes into the caller's buffers afterwards
+    auto drain = [&](int rc) {
+        (void)hipStreamSynchronize(c->bstream[0]);
+        (void)hipStreamSynchronize(c->bstream[1]);
+        return rc;
+    };
     int b = 0;
     for (uint32_t s0 = 0; s0 < n_stripes; s0 += sub, b ^= 1) {
         const uint32_t ns = std::min(sub, n_stripes - s0);
         uint8_t *dd = c->bdev[b], *dp = c->bdev[b] + size_t(sub) * dbytes;
-        HIP_TRY(hipMemcpyAsync(dd, data + size_t(s0) * dbytes, size_t(ns) * dbytes, hipMemcpyHostToDevice,
-                               c->bstream[b]));
+        hipError_t e = hipMemcpyAsync(dd, data + size_t(s0) * dbytes, size_t(ns) * dbytes, hipMemcpyHostToDevice,
+                                      c->bstream[b]);
+        if (e != hipSuccess) return drain(hip_fail(e, "hipMemcpyAsync H2D"));
         int rc = apply(c, dd, int64_t(dbytes), so, dp, int64_t(pbytes), dof, coef, ns, false, c->bstream[b]);
-        if (rc != MEC_OK) return rc;
-        HIP_TRY(hipMemcpyAsync(parity + size_t(s0) * pbytes, dp, size_t(ns) * pbytes, hipMemcpyDeviceToHost,
-                               c->bstream[b]));
+        if (rc != MEC_OK) return drain(rc);
+        e = hipMemcpyAsync(parity + size_t(s0) * pbytes, dp, size_t(ns) * pbytes, hipMemcpyDeviceToHost,
+                           c->bstream[b]);
+        if (e != hipSuccess) return drain(hip_fail(e, "hipMemcpyAsync D2H"));
     }
     HIP_TRY(hipStreamSynchronize(c->bstream[0]));
     HIP_TRY(hipStreamSynchronize(c->bstream[1]));
