@@ -120,26 +120,28 @@ __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
         for (int i = 0; i < R; ++i)
 #pragma unroll
             for (int l = 0; l < W; ++l) buf_st(acc[i * W + l], dr[i], off + l * pk);
-    } else {
-        const uint64_t off = uint64_t(u) * (4 * VW);
-        const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
-        uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
-        if (p.accumulate) {
+    } else {  // strided: chunk bases uniform per block, buffer resources as above
+        const uint32_t off = u * (4 * VW);
+        const uint32_t pk = uint32_t(p.packet);
+        const uint8_t *sb = p.src + int64_t(stripe) * p.sss;
+        uint8_t *db = p.dst + int64_t(stripe) * p.dss;
+        __amdgpu_buffer_rsrc_t dr[R];
 #pragma unroll
-            for (int i = 0; i < R; ++i)
+        for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(uint64_t(uintptr_t(db + p.dst_off[i])), p.chunk);
 #pragma unroll
-                for (int l = 0; l < W; ++l)
-                    acc[i * W + l] = ld_nt<vec>(db + p.dst_off[i] + uint64_t(l) * p.packet);
-        } else {
+        for (int i = 0; i < R; ++i)
 #pragma unroll
-            for (int r = 0; r < ROWS; ++r) acc[r] = vec(0);
+            for (int l = 0; l < W; ++l) acc[i * W + l] = p.accumulate ? buf_ld<vec>(dr[i], off + l * pk, true) : vec(0);
+        {
+            const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(uint64_t(uintptr_t(sb + p.src_off[0])), p.chunk);
+#pragma unroll
+            for (int x = 0; x < W; ++x) d[x] = buf_ld<vec>(sr, off + x * pk, true);
         }
-#pragma unroll
-        for (int x = 0; x < W; ++x) d[x] = ld_nt<vec>(sb + p.src_off[0] + uint64_t(x) * p.packet);
         for (uint32_t j = 0; j < p.k; ++j) {
             if (j + 1 < p.k) {
+                const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(uint64_t(uintptr_t(sb + p.src_off[j + 1])), p.chunk);
 #pragma unroll
-                for (int x = 0; x < W; ++x) nx[x] = ld_nt<vec>(sb + p.src_off[j + 1] + uint64_t(x) * p.packet);
+                for (int x = 0; x < W; ++x) nx[x] = buf_ld<vec>(sr, off + x * pk, true);
             }
             bm_combine<W, ROWS, vec>(d, acc, p.mask[j]);
 #pragma unroll
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
 #pragma unroll
         for (int i = 0; i < R; ++i)
 #pragma unroll
-            for (int l = 0; l < W; ++l) st_nt<vec>(db + p.dst_off[i] + uint64_t(l) * p.packet, acc[i * W + l]);
+            for (int l = 0; l < W; ++l) buf_st(acc[i * W + l], dr[i], off + l * pk);
     }
 }
 

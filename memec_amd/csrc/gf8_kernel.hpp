@@ -154,41 +154,36 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, stripe, tile);
     const uint32_t u = tile * BT + threadIdx.x;
     if (u >= p.units) return;
+    // Every chunk is a buffer resource (SGPR base, 32-bit lane offsets) in
+    // both modes: strided chunk bases are uniform per block too, and the
+    // same non-temporal stream runs 2-3 points faster through buffer
+    // instructions than through 64-bit flat addresses at the product's
+    // wave caps (tools/policy_probe.hip, profiles/r02/policy/).
+    const uint32_t off = u * 16;
+    // chunk addresses (uniform): source j / output i of this stripe
+    const uint64_t gs = p.s0 + stripe;
+    auto src_at = [&](int j) -> uint64_t {
+        if constexpr (G) return p.stab[gs * p.sstride + p.src_off[j]];
+        else return uint64_t(uintptr_t(p.src + int64_t(stripe) * p.sss + p.src_off[j]));
+    };
+    auto dst_at = [&](int i) -> uint64_t {
+        if constexpr (G) return p.dtab[gs * p.dstride + p.dst_off[i]];
+        else return uint64_t(uintptr_t(p.dst + int64_t(stripe) * p.dss + p.dst_off[i]));
+    };
     u32x4 d[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) d[j] = buf_ld<u32x4>(chunk_rsrc(src_at(j), p.chunk), off, true);
+    __amdgpu_buffer_rsrc_t dr[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(dst_at(i), p.chunk);
     u32x4 acc[R];
-    if constexpr (G) {
-        const uint32_t off = u * 16;
-        const uint64_t s = p.s0 + stripe;
-        const uint64_t *srow = p.stab + s * p.sstride;
-        const uint64_t *drow = p.dtab + s * p.dstride;
+    // read-modify-write of the outputs (delta updates) is streamed too
+    // (non-temporal: RS(10,4) update 70.9 -> 73.9 %)
 #pragma unroll
-        for (int j = 0; j < K; ++j) d[j] = buf_ld<u32x4>(chunk_rsrc(srow[p.src_off[j]], p.chunk), off, true);
-        __amdgpu_buffer_rsrc_t dr[R];
+    for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
+    gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
 #pragma unroll
-        for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(drow[p.dst_off[i]], p.chunk);
-#pragma unroll
-        for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
-        gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
-#pragma unroll
-        for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
-    } else {
-        const uint64_t off = uint64_t(u) * 16;
-        const uint8_t *sb = p.src + int64_t(stripe) * p.sss + off;
-        uint8_t *db = p.dst + int64_t(stripe) * p.dss + off;
-#pragma unroll
-        for (int j = 0; j < K; ++j) d[j] = ld_nt<u32x4>(sb + p.src_off[j]);
-        if (p.accumulate) {  // read-modify-write of the outputs, streamed too
-                             // (non-temporal: RS(10,4) update 70.9 -> 73.9 %)
-#pragma unroll
-            for (int i = 0; i < R; ++i) acc[i] = ld_nt<u32x4>(db + p.dst_off[i]);
-        } else {
-#pragma unroll
-            for (int i = 0; i < R; ++i) acc[i] = u32x4{0, 0, 0, 0};
-        }
-        gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
-#pragma unroll
-        for (int i = 0; i < R; ++i) st_nt<u32x4>(db + p.dst_off[i], acc[i]);
-    }
+    for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
 }
 
 // The < 16-byte remainder of each region (chunk sizes that are not a

@@ -387,13 +387,20 @@ const auto kGbmTable = make_gbm_table(std::make_index_sequence<8 * kMaxRows>{});
 // bench's on-box streaming ceiling.  dst may alias a or b (parity ^= delta).
 __global__ __launch_bounds__(kThreads) void xor_kernel(uint8_t *dst, const uint8_t *a, const uint8_t *b,
                                                        uint64_t len) {
+    // each block's 4 KiB span as three buffer resources (uniform bases,
+    // 32-bit lane offsets), as the coding kernels stream
     const uint64_t stride = uint64_t(gridDim.x) * kThreads * 16;
-    for (uint64_t off = (uint64_t(blockIdx.x) * kThreads + threadIdx.x) * 16; off < len; off += stride) {
-        if (off + 16 <= len) {
-            st_nt<u32x4>(dst + off, ld_nt<u32x4>(a + off) ^ ld_nt<u32x4>(b + off));
-        } else {
-            const uint32_t n = uint32_t(len - off);
-            store_partial(dst + off, load_partial(a + off, n) ^ load_partial(b + off, n), n);
+    for (uint64_t base = uint64_t(blockIdx.x) * kThreads * 16; base < len; base += stride) {
+        const uint64_t span = std::min<uint64_t>(len - base, uint64_t(kThreads) * 16);
+        const uint32_t off = threadIdx.x * 16;
+        if (off + 16 <= span) {
+            const auto ra = chunk_rsrc(uint64_t(uintptr_t(a + base)), uint32_t(span));
+            const auto rb = chunk_rsrc(uint64_t(uintptr_t(b + base)), uint32_t(span));
+            const auto rd = chunk_rsrc(uint64_t(uintptr_t(dst + base)), uint32_t(span));
+            buf_st(buf_ld<u32x4>(ra, off, true) ^ buf_ld<u32x4>(rb, off, true), rd, off);
+        } else if (off < span) {
+            const uint32_t n = uint32_t(span - off);
+            store_partial(dst + base + off, load_partial(a + base + off, n) ^ load_partial(b + base + off, n), n);
         }
     }
 }

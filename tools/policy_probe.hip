@@ -1,0 +1,137 @@
+// tools/policy_probe.hip — cache-policy bits of the stream loads and stores
+// (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16) on the RS(10,4)-shaped XOR
+// stream: 10 reads, 4 writes per 16-byte unit, dense split buffers
+// [stripe][10][1 MiB] -> [stripe][4][1 MiB], one-wave blocks over 1 KiB
+// tiles, 12 resident waves per CU (the product's encode shape), every chunk
+// a buffer resource.  The product streams with nt loads and nt stores;
+// MI355X_MICROARCH.md notes that nt / plain stores keep the line in the
+// XCD's L2 while sc1 / sc0 sc1 stores drop it.  Not part of the product.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Imemec_amd/csrc tools/policy_probe.hip -o tools/policy_probe
+//   ./tools/policy_probe [rounds=5]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "stream_common.hpp"
+
+#define CHECK(x)                                                                              \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_)); \
+            exit(1);                                                                          \
+        }                                                                                     \
+    } while (0)
+
+using namespace mec::detail;
+
+constexpr int K = 10, R = 4;
+constexpr uint64_t CS = 1 << 20;
+constexpr uint32_t TPS = uint32_t(CS / 1024);
+
+template <int LA, int SA>
+__global__ __launch_bounds__(64) void k_policy(const uint8_t *src, uint8_t *dst) {
+    const uint32_t stripe = blockIdx.x / TPS, t = blockIdx.x % TPS;
+    const uint32_t off = t * 1024 + threadIdx.x * 16;
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(src + (uint64_t(stripe) * K + j) * CS),
+                                                         0, int(CS), 0x00020000);
+        x[j] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, LA);
+    }
+    u32x4 acc = x[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) acc ^= x[j];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(dst + (uint64_t(stripe) * R + i) * CS, 0, int(CS), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(acc + u32x4{uint32_t(i), 0, 0, 0}, r, off, 0, SA);
+    }
+}
+
+// the product's flat non-temporal version, for reference
+__global__ __launch_bounds__(64) void k_flat(const uint8_t *src, uint8_t *dst) {
+    const uint32_t stripe = blockIdx.x / TPS, t = blockIdx.x % TPS;
+    const uint64_t off = uint64_t(t) * 1024 + threadIdx.x * 16;
+    const uint8_t *s = src + uint64_t(stripe) * K * CS + off;
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = ld_nt<u32x4>(s + j * CS);
+    u32x4 acc = x[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) acc ^= x[j];
+    uint8_t *d = dst + uint64_t(stripe) * R * CS + off;
+#pragma unroll
+    for (int i = 0; i < R; ++i) st_nt<u32x4>(d + i * CS, acc + u32x4{uint32_t(i), 0, 0, 0});
+}
+
+typedef void (*Launch)(const uint8_t *, uint8_t *, uint32_t, size_t, hipStream_t);
+template <int LA, int SA>
+void launch(const uint8_t *s, uint8_t *d, uint32_t stripes, size_t lds, hipStream_t st) {
+    hipLaunchKernelGGL((k_policy<LA, SA>), dim3(stripes * TPS), dim3(64), lds, st, s, d);
+}
+void launch_flat(const uint8_t *s, uint8_t *d, uint32_t stripes, size_t lds, hipStream_t st) {
+    hipLaunchKernelGGL(k_flat, dim3(stripes * TPS), dim3(64), lds, st, s, d);
+}
+
+int main(int argc, char **argv) {
+    const int rounds = argc > 1 ? atoi(argv[1]) : 5;
+    const uint32_t stripes = 2048;  // 28 GiB moved per launch
+    uint8_t *src, *dst;
+    CHECK(hipMalloc(&src, size_t(stripes) * K * CS));
+    CHECK(hipMalloc(&dst, size_t(stripes) * R * CS));
+    CHECK(hipMemset(src, 0x3c, size_t(stripes) * K * CS));
+    hipStream_t st;
+    CHECK(hipStreamCreate(&st));
+    struct Arm {
+        const char *name;
+        Launch fn;
+    };
+    const Arm arms[] = {
+        {"flat nt / nt (product)", launch_flat},
+        {"buf  nt / nt", launch<2, 2>},
+        {"buf  nt / plain", launch<2, 0>},
+        {"buf  nt / sc1", launch<2, 16>},
+        {"buf  nt / sc0 sc1", launch<2, 17>},
+        {"buf  nt / nt sc1", launch<2, 18>},
+        {"buf  plain / nt", launch<0, 2>},
+        {"buf  sc1 / nt", launch<16, 2>},
+        {"buf  nt sc1 / nt sc1", launch<18, 18>},
+        {"buf  plain / plain", launch<0, 0>},
+    };
+    const int na = sizeof(arms) / sizeof(arms[0]);
+    const uint32_t caps[] = {12, 16, 0};
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    const double bytes = double(stripes) * (K + R) * CS;
+    for (uint32_t cap : caps) {
+        const size_t lds = cap ? ((160u << 10) / cap / 512 * 512 - 512) : 0;
+        std::vector<std::vector<float>> ms(na);
+        for (int r = 0; r < rounds; ++r)
+            for (int i = 0; i < na; ++i) {
+                arms[i].fn(src, dst, stripes, lds, st);
+                CHECK(hipEventRecord(e0, st));
+                for (int q = 0; q < 5; ++q) arms[i].fn(src, dst, stripes, lds, st);
+                CHECK(hipEventRecord(e1, st));
+                CHECK(hipEventSynchronize(e1));
+                float t = 0;
+                CHECK(hipEventElapsedTime(&t, e0, e1));
+                ms[i].push_back(t / 5);
+            }
+        printf("%u waves/CU cap (0 = none), %.2f GB per launch, median of %d x 5\n", cap, bytes / 1e9, rounds);
+        for (int i = 0; i < na; ++i) {
+            std::sort(ms[i].begin(), ms[i].end());
+            const double med = ms[i][ms[i].size() / 2];
+            printf("  %-24s %7.1f GB/s %5.1f %%\n", arms[i].name, bytes / (med * 1e-3) / 1e9,
+                   bytes / (med * 1e-3) / 8e12 * 100);
+        }
+        fflush(stdout);
+    }
+    return 0;
+}
