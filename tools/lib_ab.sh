@@ -3,7 +3,7 @@
 # memec_amd/libmec.so (new) against memec_amd/libmec_<OLD>.so, bench.py
 # lines per config, ROUNDS alternations.  Restores the new build at the end.
 # Not product code.
-#   OLD=flat CFGS="rs_enc rs_dec" ROUNDS=2 bash tools/lib_ab.sh
+#   OLD=flat CFGS="rs_enc rs_dec" ROUNDS=2 EXTRA="--stripes 32768" bash tools/lib_ab.sh
 set -u
 cd "$(dirname "$0")/.."
 OLD=${OLD:-flat}
@@ -16,7 +16,7 @@ for r in $(seq 1 "$ROUNDS"); do
     for v in new "$OLD"; do
         if [ "$v" = new ]; then cp /tmp/libmec_new.so memec_amd/libmec.so; else cp "memec_amd/libmec_$v.so" memec_amd/libmec.so; fi
         for c in $CFGS; do
-            timeout -k 10 200 python bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 20 \
+            timeout -k 10 200 python bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 20 ${EXTRA:-} \
                 > "gpurun_out/lib_ab/${v}_${c}_$r.json" 2> "gpurun_out/lib_ab/${v}_${c}_$r.err" || { rc=$?; break 3; }
             python - "$v" "$c" "$r" <<'PY'
 import json, sys
