@@ -45,11 +45,16 @@ template <>
 __device__ __forceinline__ u32x2 buf_ld<u32x2>(__amdgpu_buffer_rsrc_t r, uint32_t off, bool nt) {
     return nt ? __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxNT) : __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
 }
+// Stores: non-temporal + sc1 (the line leaves the XCD's L2 instead of
+// staying in it): the in-place RS(10,4)-shaped stream +0.7-1.4 points at
+// 12-20 waves per CU, split layouts unchanged (tools/policy_probe.hip,
+// profiles/r02/policy/policy_probe_inplace.log).
+constexpr int kAuxStore = 2 | 16;
 __device__ __forceinline__ void buf_st(u32x4 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxNT);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, kAuxStore);
 }
 __device__ __forceinline__ void buf_st(u32x2 v, __amdgpu_buffer_rsrc_t r, uint32_t off) {
-    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, kAuxNT);
+    __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, kAuxStore);
 }
 
 // An SGPR zero the compiler cannot see through: offsetting the LDS table

@@ -70,6 +70,46 @@ __global__ __launch_bounds__(64) void k_flat(const uint8_t *src, uint8_t *dst) {
     for (int i = 0; i < R; ++i) st_nt<u32x4>(d + i * CS, acc + u32x4{uint32_t(i), 0, 0, 0});
 }
 
+// in place, as the RS(10,4) decode of {0,1,2,3}: [stripe][14][1 MiB], read
+// chunks 4..13, write chunks 0..3; 4-wave blocks over 4 KiB tiles, grid cut
+// into 2 windows taken round-robin (stream_common.hpp block_order)
+constexpr uint32_t TPS4 = uint32_t(CS / 4096);
+template <int LA, int SA>
+__global__ __launch_bounds__(256) void k_inplace(uint8_t *buf) {
+    const uint32_t bid = block_order(2);
+    const uint32_t stripe = bid / TPS4, t = bid % TPS4;
+    const uint32_t off = t * 4096 + threadIdx.x * 16;
+    uint8_t *sb = buf + uint64_t(stripe) * (K + R) * CS;
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(sb + (R + j) * CS, 0, int(CS), 0x00020000);
+        x[j] = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, LA);
+    }
+    u32x4 acc = x[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) acc ^= x[j];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+        const auto r = __builtin_amdgcn_make_buffer_rsrc(sb + i * CS, 0, int(CS), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(acc + u32x4{uint32_t(i), 0, 0, 0}, r, off, 0, SA);
+    }
+}
+__global__ __launch_bounds__(256) void k_inplace_flat(uint8_t *buf) {
+    const uint32_t bid = block_order(2);
+    const uint32_t stripe = bid / TPS4, t = bid % TPS4;
+    const uint64_t off = uint64_t(t) * 4096 + threadIdx.x * 16;
+    uint8_t *sb = buf + uint64_t(stripe) * (K + R) * CS + off;
+    u32x4 x[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) x[j] = ld_nt<u32x4>(sb + (R + j) * CS);
+    u32x4 acc = x[0];
+#pragma unroll
+    for (int j = 1; j < K; ++j) acc ^= x[j];
+#pragma unroll
+    for (int i = 0; i < R; ++i) st_nt<u32x4>(sb + i * CS, acc + u32x4{uint32_t(i), 0, 0, 0});
+}
+
 typedef void (*Launch)(const uint8_t *, uint8_t *, uint32_t, size_t, hipStream_t);
 template <int LA, int SA>
 void launch(const uint8_t *s, uint8_t *d, uint32_t stripes, size_t lds, hipStream_t st) {
@@ -77,6 +117,14 @@ void launch(const uint8_t *s, uint8_t *d, uint32_t stripes, size_t lds, hipStrea
 }
 void launch_flat(const uint8_t *s, uint8_t *d, uint32_t stripes, size_t lds, hipStream_t st) {
     hipLaunchKernelGGL(k_flat, dim3(stripes * TPS), dim3(64), lds, st, s, d);
+}
+// in-place arms: `d` is the [stripe][14][CS] buffer (its first part), `stripes` of them
+template <int LA, int SA>
+void launch_ip(const uint8_t *, uint8_t *d, uint32_t stripes, size_t lds, hipStream_t st) {
+    hipLaunchKernelGGL((k_inplace<LA, SA>), dim3(stripes * TPS4), dim3(256), lds, st, d);
+}
+void launch_ip_flat(const uint8_t *, uint8_t *d, uint32_t stripes, size_t lds, hipStream_t st) {
+    hipLaunchKernelGGL(k_inplace_flat, dim3(stripes * TPS4), dim3(256), lds, st, d);
 }
 
 int main(int argc, char **argv) {
@@ -110,7 +158,7 @@ int main(int argc, char **argv) {
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
     const double bytes = double(stripes) * (K + R) * CS;
-    for (uint32_t cap : caps) {
+    for (uint32_t cap : (getenv("PP_INPLACE_ONLY") ? std::vector<uint32_t>{} : std::vector<uint32_t>(caps, caps + 3))) {
         const size_t lds = cap ? ((160u << 10) / cap / 512 * 512 - 512) : 0;
         std::vector<std::vector<float>> ms(na);
         for (int r = 0; r < rounds; ++r)
@@ -130,6 +178,44 @@ int main(int argc, char **argv) {
             const double med = ms[i][ms[i].size() / 2];
             printf("  %-24s %7.1f GB/s %5.1f %%\n", arms[i].name, bytes / (med * 1e-3) / 1e9,
                    bytes / (med * 1e-3) / 8e12 * 100);
+        }
+        fflush(stdout);
+    }
+    // in-place arms over one [stripe][14][1 MiB] buffer (the src allocation
+    // holds 2048 x 10 MiB; 1462 stripes of 14 MiB fit)
+    const uint32_t ipn = uint32_t(size_t(stripes) * K / (K + R)) / 2 * 2;
+    const Arm ip[] = {
+        {"in place flat nt / nt", launch_ip_flat},
+        {"in place buf nt / nt", launch_ip<2, 2>},
+        {"in place buf nt / nt sc1", launch_ip<2, 18>},
+        {"in place buf nt / sc1", launch_ip<2, 16>},
+        {"in place buf nt sc1 / nt sc1", launch_ip<18, 18>},
+        {"in place buf nt / plain", launch_ip<2, 0>},
+    };
+    const int ni = sizeof(ip) / sizeof(ip[0]);
+    const double ibytes = double(ipn) * (K + R) * CS;
+    for (uint32_t cap : {16u, 12u, 20u, 0u}) {
+        // 4-wave blocks: LDS per block so that cap/4 blocks share a CU
+        const uint32_t blocks = cap ? std::max<uint32_t>(1, cap / 4) : 0;
+        const size_t lds = blocks ? ((160u << 10) / blocks / 512 * 512 - 512) : 0;
+        std::vector<std::vector<float>> ms(ni);
+        for (int r = 0; r < rounds; ++r)
+            for (int i = 0; i < ni; ++i) {
+                ip[i].fn(nullptr, src, ipn, lds, st);
+                CHECK(hipEventRecord(e0, st));
+                for (int q = 0; q < 5; ++q) ip[i].fn(nullptr, src, ipn, lds, st);
+                CHECK(hipEventRecord(e1, st));
+                CHECK(hipEventSynchronize(e1));
+                float t = 0;
+                CHECK(hipEventElapsedTime(&t, e0, e1));
+                ms[i].push_back(t / 5);
+            }
+        printf("in place, %u waves/CU cap (0 = none), %u stripes, %.2f GB per launch\n", cap, ipn, ibytes / 1e9);
+        for (int i = 0; i < ni; ++i) {
+            std::sort(ms[i].begin(), ms[i].end());
+            const double med = ms[i][ms[i].size() / 2];
+            printf("  %-30s %7.1f GB/s %5.1f %%\n", ip[i].name, ibytes / (med * 1e-3) / 1e9,
+                   ibytes / (med * 1e-3) / 8e12 * 100);
         }
         fflush(stdout);
     }
