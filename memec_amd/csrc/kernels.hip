@@ -385,13 +385,13 @@ const auto kGbmTable = make_gbm_table(std::make_index_sequence<8 * kMaxRows>{});
 // One 16-byte unit per lane over the whole region (grid-stride only past
 // 16 GiB), non-temporal: a plain 2-read / 1-write HBM stream, also the
 // bench's on-box streaming ceiling.  dst may alias a or b (parity ^= delta).
-__global__ __launch_bounds__(kThreads) void xor_kernel(uint8_t *dst, const uint8_t *a, const uint8_t *b,
-                                                       uint64_t len) {
-    // each block's 4 KiB span as three buffer resources (uniform bases,
-    // 32-bit lane offsets), as the coding kernels stream
-    const uint64_t stride = uint64_t(gridDim.x) * kThreads * 16;
-    for (uint64_t base = uint64_t(blockIdx.x) * kThreads * 16; base < len; base += stride) {
-        const uint64_t span = std::min<uint64_t>(len - base, uint64_t(kThreads) * 16);
+template <int BT>
+__global__ __launch_bounds__(BT) void xor_kernel(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len) {
+    // each block's BT x 16-byte span as three buffer resources (uniform
+    // bases, 32-bit lane offsets), as the coding kernels stream
+    const uint64_t stride = uint64_t(gridDim.x) * BT * 16;
+    for (uint64_t base = uint64_t(blockIdx.x) * BT * 16; base < len; base += stride) {
+        const uint64_t span = std::min<uint64_t>(len - base, uint64_t(BT) * 16);
         const uint32_t off = threadIdx.x * 16;
         if (off + 16 <= span) {
             const auto ra = chunk_rsrc(uint64_t(uintptr_t(a + base)), uint32_t(span));
@@ -465,11 +465,17 @@ hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream) {
 
 hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, hipStream_t stream) {
     if (len == 0) return hipSuccess;
-    const uint64_t units = (len + 15) / 16, blocks = (units + kThreads - 1) / kThreads;
-    // 2 source streams + 1 output per lane: the gf8 split-layout rule
-    const uint32_t lds = occupancy_lds(kThreads, kThreads, 0, gf8_target_waves(2, 1, false, false, false));
-    hipLaunchKernelGGL(xor_kernel, dim3(uint32_t(std::min<uint64_t>(blocks, uint64_t(1) << 22))), dim3(kThreads), lds,
-                       stream, dst, a, b, len);
+    // one-wave blocks over 1 KiB tiles unless MEC_BLOCK=256, like the
+    // split-layout coding launches; 2 source streams + 1 output per lane:
+    // the gf8 split-layout cap
+    const uint32_t bt = block_threads(true, 1, false);
+    const uint64_t units = (len + 15) / 16, blocks = (units + bt - 1) / bt;
+    const uint32_t lds = occupancy_lds(bt, bt, 0, gf8_target_waves(2, 1, false, false, false));
+    const dim3 grid(uint32_t(std::min<uint64_t>(blocks, uint64_t(1) << 24)));
+    if (bt == kWaveBlock)
+        hipLaunchKernelGGL((xor_kernel<kWaveBlock>), grid, dim3(bt), lds, stream, dst, a, b, len);
+    else
+        hipLaunchKernelGGL((xor_kernel<kThreads>), grid, dim3(bt), lds, stream, dst, a, b, len);
     return hipGetLastError();
 }
 
