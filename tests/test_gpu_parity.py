@@ -350,8 +350,26 @@ def test_host_batch_encode():
 
 
 def test_xor():
-    for n in [1, 15, 16, 4097, 1 << 20]:
+    # partial 16-byte units, partial one-wave tiles (1 KiB), aligned sizes
+    for n in [1, 15, 16, 1023, 1025, 1040, 4097, (1 << 20) + 7, 1 << 20]:
         a, b = dev_fill(n, 1), dev_fill(n, 2)
         d = torch.empty_like(a)
         xor(d, a, b)
         assert np.array_equal(to_np(d), O.fill(n, 1) ^ O.fill(n, 2)), n
+    # dst aliasing a source (parity ^= delta, Coding::bitwiseXOR's use)
+    a, b = dev_fill(5000, 3), dev_fill(5000, 4)
+    xor(a, a, b)
+    assert np.array_equal(to_np(a), O.fill(5000, 3) ^ O.fill(5000, 4))
+
+
+def test_xor_grid_stride_past_16_gib():
+    """Past 2^24 one-wave tiles (16 GiB) the launch strides its grid; the
+    tail tile is partial too."""
+    n = (16 << 30) + 4096 + 3
+    a, b = dev_fill(n, 5), dev_fill(n, 6)
+    d = torch.empty_like(a)
+    xor(d, a, b)
+    torch.bitwise_xor(a, b, out=a)
+    assert torch.equal(d, a)
+    del a, b, d
+    torch.cuda.empty_cache()
