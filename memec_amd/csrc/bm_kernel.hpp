@@ -175,10 +175,17 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
     // the bitmatrix kernel 3.5 % on aligned decode batches), unaligned ones
     // take the capped 4-wave shape (+1-3 %; profiles/r02/host/gather_ab_bm.log)
     const uint8_t gshape = L.gshape == 1 ? 0 : L.gshape;
+    // one-wave blocks in place: chunks of kBmWaveChunk or more, and
+    // 16-32 KiB chunks with <= 2 output rows and k >= 6 (8-byte lanes, 12
+    // waves per CU; CRS(6,2) / (8,2) / (12,2) in place +1-5 points,
+    // CRS(4,2), CRS(12,4), 8 KiB and >= 64 KiB chunks lose;
+    // profiles/r02/bmshape/)
+    const uint64_t cb = uint64_t(p.chunk);
+    const bool wave_ip = cb >= kBmWaveChunk || (R <= 2 && L.k >= 6 && cb >= (16u << 10) && cb <= (32u << 10));
     const uint32_t bt = L.stab ? gathered_block_threads(gshape)
                                : block_threads(true, launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
                                                                     int64_t(L.n_stripes) * L.dst_stripe_stride),
-                                               uint64_t(p.chunk) >= kBmWaveChunk);
+                                               wave_ip);
     const Geometry g = geometry(L.packet / UB, bt);
     p.units = g.units;
     p.tiles = g.tiles;
