@@ -77,22 +77,23 @@ def cpu_baseline(fam, k, m, cs, gpu_parity_np, seed, threads):
     import _oracle as O
 
     per = k * cs
-    sample = max(threads, min(64, (768 << 20) // ((k + m) * cs)))
-    sample = (sample // threads) * threads or threads
+    sample = cpu_sample(k, m, cs, threads)
+    p = cpu_parallelism(threads, host_cores()[0], sample)
+    log("cpu_baseline encode: port, %d stripes on %d threads" % (sample, threads))
     data = O.fill(sample * per, seed)
     par = np.zeros(sample * m * cs, np.uint8)
-    # 1 thread, 1 pass over `threads` stripes (single-core figure)
+    # 1 thread, 1 pass over `p` stripes (single-core figure)
     t0 = time.perf_counter()
-    O.encode_batch_mt(fam, k, m, cs, data, par, threads, 1)
+    O.encode_batch_mt(fam, k, m, cs, data, par, p, 1)
     t1 = time.perf_counter()
-    single = threads * per / (t1 - t0) / 2**30
-    passes, t_total, reps = 0, 0.0, 0
+    single = p * per / (t1 - t0) / 2**30
+    passes, t_total = 0, 0.0
     t0 = time.perf_counter()
     while True:
         O.encode_batch_mt(fam, k, m, cs, data, par, sample, threads)
         passes += 1
         t_total = time.perf_counter() - t0
-        if t_total * threads >= 10.0 or passes >= 64:
+        if t_total * p >= CPU_WORK_S[0] or passes >= 64:
             break
     value = passes * sample * per / t_total / 2**30
     verified = None
@@ -131,9 +132,53 @@ def _ref_lib():
     return L
 
 
-def ref_baseline(fam, k, m, cs, threads, sample, run):
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    sys.stderr.write("bench: %s\n" % msg)
+    sys.stderr.flush()
+
+
+# CPU-baseline samples are sized by bytes, never by the thread count: a
+# --cpu-threads far above the host's cores once asked for 256 stripes of
+# 14 MiB per leg and ~512 CPU-seconds of reference work, which the GPU
+# box's output watchdog killed (profiles/r02/cpu/cpu_threads_ab.log).
+CPU_SAMPLE_BYTES = 768 << 20      # stripe bytes ((k + m) * chunk) per leg
+CPU_SAMPLE_BYTES_MAX = 1 << 30    # ... when more stripes are needed to give every thread one
+CPU_WORK_S = (10.0, 30.0)         # CPU-seconds of reference work per leg (min, max)
+
+
+def cpu_sample(k, m, cs, threads):
+    """Stripes in one CPU-baseline leg: ~768 MiB (1 to 64 stripes), raised
+    to one stripe per thread while that stays under 1 GiB, and a multiple
+    of the threads that get work."""
+    sb = (k + m) * cs
+    base = max(1, min(64, CPU_SAMPLE_BYTES // sb))
+    hi = max(base, CPU_SAMPLE_BYTES_MAX // sb)
+    n = min(max(base, threads), hi)
+    t = max(1, min(threads, n))
+    return n // t * t
+
+
+def cpu_parallelism(threads, usable, sample):
+    """Workers that actually run at once: requested threads, capped by the
+    host's usable cores (cgroup quota / affinity) and the sample's stripes."""
+    return max(1, min(threads, usable, sample))
+
+
+def cpu_work_plan(probe_s, threads, usable, sample):
+    """Passes of a timed CPU leg whose single-worker pass over the sample
+    took probe_s: 10-30 CPU-seconds of work (2 s per running worker), so
+    the wall time stays ~10 s at one core and ~2 s at 16 whatever the
+    requested thread count.  Returns (passes, estimated wall seconds)."""
+    p = cpu_parallelism(threads, usable, sample)
+    cpu_s = min(CPU_WORK_S[1], max(CPU_WORK_S[0], 2.0 * p))
+    passes = int(max(1, min(4096, round(cpu_s / max(probe_s, 1e-6)))))
+    return passes, passes * probe_s / p
+
+
+def ref_baseline(fam, k, m, cs, threads, sample, run, usable=None, label=""):
     """Time the compiled reference on `sample` stripes: a single-worker
-    probe pass, then enough passes for ~10 s of CPU work (<= 4096).
+    probe pass, then the passes of cpu_work_plan on `threads` workers.
     run(L, h, passes, n_stripes, threads) -> seconds."""
     L = _ref_lib()
     if L is None or fam not in ("rs", "cauchy"):
@@ -141,11 +186,12 @@ def ref_baseline(fam, k, m, cs, threads, sample, run):
     h = L.ref_instantiate(4 if fam == "rs" else 7, k, m, cs)  # CS_RS / CS_CAUCHY
     if not h:
         return None
+    usable = usable or host_cores()[0]
     try:
         probe = run(L, h, 1, sample, 1)  # one worker, one pass over the sample
-        # >= 10 s of CPU work and >= ~2 s of wall time on `threads` workers
-        cpu_s = max(10.0, 2.0 * threads)
-        passes = int(max(1, min(4096, round(cpu_s / max(probe, 1e-6)))))
+        passes, est = cpu_work_plan(probe, threads, usable, sample)
+        log("cpu_baseline %s: reference, %d stripes x %d passes on %d threads (%d usable cores), ~%.1f s"
+            % (label, sample, passes, threads, usable, est))
         dt = run(L, h, passes, sample, threads)
     finally:
         L.ref_destroy(h)
@@ -161,7 +207,7 @@ def cpu_baseline_reference(fam, k, m, cs, gpu_parity_np, seed, threads, op, eras
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
 
-    sample = decode_sample(k, m, cs, threads)
+    sample = cpu_sample(k, m, cs, threads)
     per = k * cs
     if op == "encode":
         data = O.fill(sample * per, seed)
@@ -175,7 +221,7 @@ def cpu_baseline_reference(fam, k, m, cs, gpu_parity_np, seed, threads, op, eras
 
         def run(L, h, passes, n, t):
             return L.ref_decode_batch_mt(h, buf.ctypes.data, n, present, t, passes)
-    r = ref_baseline(fam, k, m, cs, threads, sample, run)
+    r = ref_baseline(fam, k, m, cs, threads, sample, run, label=op)
     if r is None:
         return None
     probe, passes, dt = r
@@ -210,8 +256,7 @@ def cpu_baseline_reference_update(fam, k, m, cs, j, threads):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
 
-    sample = max(threads, min(256, (768 << 20) // ((k + 2 * m) * cs)))
-    sample = (sample // threads) * threads or threads
+    sample = cpu_sample(k, m, cs, threads)
     delta = O.fill(sample * cs, 5)
     par0 = O.fill(sample * m * cs, 6)
     par = par0.copy()
@@ -221,7 +266,7 @@ def cpu_baseline_reference_update(fam, k, m, cs, j, threads):
     def run(L, h, passes, n, t):
         applied[:n] += passes
         return L.ref_update_batch_mt(h, delta.ctypes.data, par.ctypes.data, j, n, t, passes)
-    r = ref_baseline(fam, k, m, cs, threads, sample, run)
+    r = ref_baseline(fam, k, m, cs, threads, sample, run, label="update")
     if r is None:
         return None
     probe, passes, dt = r
@@ -245,11 +290,6 @@ def cpu_baseline_reference_update(fam, k, m, cs, j, threads):
             "cpu_model": cpu_model()}
 
 
-def decode_sample(k, m, cs, threads):
-    sample = max(threads, min(64, (768 << 20) // ((k + m) * cs)))
-    return (sample // threads) * threads or threads
-
-
 def cpu_baseline_decode(fam, k, m, cs, erased, codewords, threads):
     """Oracle decode (jerasure_matrix_decode / schedule decode restated,
     decoding matrix rebuilt per stripe as the reference does per call) on a
@@ -264,16 +304,18 @@ def cpu_baseline_decode(fam, k, m, cs, erased, codewords, threads):
     view = buf.reshape(sample, k + m, cs)
     view[:, erased] = 0
     per = k * cs
+    p = cpu_parallelism(threads, host_cores()[0], sample)
+    log("cpu_baseline decode: port, %d stripes on %d threads" % (sample, threads))
     t0 = time.perf_counter()
-    O.decode_batch_mt(fam, k, m, cs, buf, threads, erased, 1)
-    single = threads * per / (time.perf_counter() - t0) / 2**30
+    O.decode_batch_mt(fam, k, m, cs, buf, p, erased, 1)
+    single = p * per / (time.perf_counter() - t0) / 2**30
     passes = 0
     t0 = time.perf_counter()
     while True:
         rc = O.decode_batch_mt(fam, k, m, cs, buf, sample, erased, threads)
         passes += 1
         t_total = time.perf_counter() - t0
-        if rc != 0 or t_total * threads >= 10.0 or passes >= 64:
+        if rc != 0 or t_total * p >= CPU_WORK_S[0] or passes >= 64:
             break
     value = passes * sample * per / t_total / 2**30
     return {"value": round(value, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
@@ -294,8 +336,9 @@ def cpu_baseline_update(fam, k, m, cs, j, threads):
     import numpy as np
     import _oracle as O
 
-    sample = max(threads, min(256, (768 << 20) // ((k + 2 * m) * cs)))
-    sample = (sample // threads) * threads or threads
+    sample = cpu_sample(k, m, cs, threads)
+    p = cpu_parallelism(threads, host_cores()[0], sample)
+    log("cpu_baseline update: port, %d stripes on %d threads" % (sample, threads))
     data = np.zeros((sample, k, cs), np.uint8)
     data[:, j] = O.fill(sample * cs, 5).reshape(sample, cs)
     data = data.reshape(-1)
@@ -308,13 +351,184 @@ def cpu_baseline_update(fam, k, m, cs, j, threads):
         np.bitwise_xor(parity, delta_par, out=parity)
         passes += 1
         t_total = time.perf_counter() - t0
-        if t_total * threads >= 10.0 or passes >= 64:
+        if t_total * p >= CPU_WORK_S[0] or passes >= 64:
             break
     value = passes * sample * cs / t_total / 2**30
     return {"value": round(value, 4), "unit": "GiB/s (delta bytes)", "cores": threads, "kind": "port",
             "sample": "%d stripes x %d passes: orc_encode_batch_mt over the zero-padded delta stripe + XOR "
                       "into parity (numpy), %d threads" % (sample, passes, threads),
             "matches_gpu": None, "cpu_model": cpu_model()}
+
+
+# ---- parity pins: sampled GPU outputs against the reference itself ----------
+# Every config the bench times is checked here, outside the timed region, on
+# stripes spread over the whole batch, against oracle/_ref (MemEC's own
+# Coding::encode / Coding::decode compiled from the reference sources; the
+# oracle port when that library did not travel) — the reference's checker
+# re-encodes and memcmps the same way (test/common/coding/checker.cc:132-164).
+# Decode batches also carry random NON-codeword stripes: their "rebuilt"
+# chunks depend on exactly which survivors and which decoding matrix the
+# decoder uses (jerasure.c:98-126, 167-268), so equality there pins the
+# survivor choice, which a round trip of codewords cannot.
+REF_VS = "oracle/_ref (MemEC Coding::%s compiled from the reference sources)"
+PORT_VS = "oracle/oracle.c (restatement; oracle/_ref absent)"
+PARITY_BYTES = 192 << 20  # stripe bytes per sampled set
+
+
+def parity_count(k, m, cs):
+    """Stripes per sampled set: ~192 MiB of stripe bytes, 4 to 64."""
+    return int(max(4, min(64, PARITY_BYTES // ((k + m) * cs))))
+
+
+def spread(lo, hi, n):
+    """Up to n distinct indices spread evenly over [lo, hi), both ends
+    included."""
+    n = max(0, min(n, hi - lo))
+    if n <= 1:
+        return [lo] if n == 1 else []
+    return sorted({lo + (hi - 1 - lo) * i // (n - 1) for i in range(n)})
+
+
+def ref_encode(fam, k, m, cs, data, threads=1):
+    """data [n][k][cs] uint8 -> (the reference's parity [n][m][cs], source)."""
+    import numpy as np
+    data = np.ascontiguousarray(data)
+    n = data.shape[0]
+    par = np.zeros((n, m, cs), np.uint8)
+    L = _ref_lib() if fam in ("rs", "cauchy") else None
+    h = L.ref_instantiate(4 if fam == "rs" else 7, k, m, cs) if L is not None else None
+    if h:
+        try:
+            L.ref_encode_batch_mt(h, data.ctypes.data, par.ctypes.data, n, max(1, min(threads, n)), 1)
+        finally:
+            L.ref_destroy(h)
+        return par, REF_VS % "encode"
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    for s_ in range(n):
+        par[s_] = np.stack(O.encode(fam, k, m, [data[s_, j].copy() for j in range(k)], cs))
+    return par, PORT_VS
+
+
+def ref_decode(fam, k, m, cs, stripes, erased, threads=1):
+    """stripes [n][k+m][cs] (the erased chunks' bytes are ignored: cleared
+    first, as server_peer_res_worker.cc:818-828 clears them) -> (the
+    reference's rebuilt stripes, source)."""
+    import numpy as np
+    buf = np.ascontiguousarray(stripes).copy()
+    n = buf.shape[0]
+    buf[:, erased] = 0
+    present = sum(1 << i for i in range(k + m) if i not in erased)
+    L = _ref_lib() if fam in ("rs", "cauchy") else None
+    h = L.ref_instantiate(4 if fam == "rs" else 7, k, m, cs) if L is not None else None
+    if h:
+        try:
+            rc = L.ref_decode_batch_mt(h, buf.ctypes.data, n, present, max(1, min(threads, n)), 1)
+        finally:
+            L.ref_destroy(h)
+        if rc < 0:
+            raise RuntimeError("reference decode returned false")
+        return buf, REF_VS % "decode"
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    for s_ in range(n):
+        chunks = [buf[s_, i].copy() for i in range(k + m)]
+        if O.decode(fam, k, m, chunks, erased, cs) != 0:
+            raise RuntimeError("oracle decode failed")
+        buf[s_] = np.stack(chunks)
+    return buf, PORT_VS
+
+
+def _rows(t, idx):
+    """Stripes idx of a [n, ...] CUDA tensor as a numpy array."""
+    import torch
+    return t[torch.tensor(idx, dtype=torch.long, device=t.device)].cpu().numpy()
+
+
+def check_encode(fam, k, m, cs, data, parity, threads=1):
+    """Sampled stripes of a GPU encode (data [n][k][cs], parity [n][m][cs]
+    CUDA tensors) against the reference's encode of the same stripes."""
+    import numpy as np
+    idx = spread(0, data.shape[0], parity_count(k, m, cs))
+    want, vs = ref_encode(fam, k, m, cs, _rows(data, idx), threads)
+    return {"vs": vs, "stripes": len(idx), "equal": bool(np.array_equal(_rows(parity, idx), want)),
+            "sample": "%d stripes spread over [0, %d)" % (len(idx), data.shape[0])}
+
+
+def plant_noncodewords(st, k, m, cs, seed):
+    """Before a decode: overwrite stripes spread over the second half of
+    `st` ([n][k+m][cs] CUDA tensor of codewords) with random bytes in every
+    chunk, and keep host copies of those and of codeword stripes spread
+    over the first half.  Returns the record check_decode needs."""
+    import torch
+    n = st.shape[0]
+    cnt = parity_count(k, m, cs)
+    nc = spread(n // 2, n, cnt) if n >= 2 else []
+    cw = spread(0, max(1, n // 2), cnt)
+    rec = {"nc": nc, "cw": cw, "cw_np": _rows(st, cw), "nc_np": None}
+    if nc:
+        from memec_amd import fill_random
+        noise = torch.empty(len(nc), k + m, cs, dtype=torch.uint8, device=st.device)
+        if st.is_cuda:
+            fill_random(noise, seed)
+        else:  # CPU tests of this harness (tests/test_bench_baseline.py)
+            noise.copy_(torch.randint(0, 256, noise.shape, dtype=torch.uint8,
+                                      generator=torch.Generator().manual_seed(seed)))
+        st[torch.tensor(nc, dtype=torch.long, device=st.device)] = noise
+        rec["nc_np"] = noise.cpu().numpy()
+    return rec
+
+
+def check_decode(fam, k, m, cs, st, erased, rec, threads=1):
+    """After a GPU decode of `st` (in place): the sampled codeword and
+    non-codeword stripes, whole, against the reference's decode of the
+    same stripes with the same erasures."""
+    import numpy as np
+    eq, vs = True, None
+    for idx, before in ((rec["cw"], rec["cw_np"]), (rec["nc"], rec["nc_np"])):
+        if not idx:
+            continue
+        want, vs = ref_decode(fam, k, m, cs, before, erased, threads)
+        eq = eq and bool(np.array_equal(_rows(st, idx), want))
+    return {"vs": vs, "codeword_stripes": len(rec["cw"]), "non_codeword_stripes": len(rec["nc"]),
+            "erased": list(erased), "equal": eq,
+            "sample": "codewords spread over the first half of %d stripes, random non-codewords over the second"
+                      % st.shape[0]}
+
+
+def restore_noncodewords(st, saved, erased, rec):
+    """`saved` holds the erased chunks of the original codewords: the
+    non-codeword stripes' chunks are replaced by the GPU's own output there,
+    so a whole-batch round-trip check covers every other stripe."""
+    import torch
+    if rec["nc"]:
+        t = torch.tensor(rec["nc"], dtype=torch.long, device=st.device)
+        saved[t] = st[t][:, erased]
+
+
+def twin_rate(codec, step, alg_bytes, reps=5):
+    """The same launch with every GF(2^8) product a plain XOR
+    (mec_set_probe): best of `reps` launches, GB/s of the same algorithmic
+    bytes.  The outputs are garbage afterwards.  None for Cauchy-RS."""
+    import torch
+    if codec.family == "cauchy":
+        return None
+    codec.set_probe(True)
+    try:
+        step()
+        torch.cuda.synchronize()
+        best = None
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            step()
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+    finally:
+        codec.set_probe(False)
+    return alg_bytes / (best * 1e-3) / 1e9
 
 
 def cpu_model():
@@ -329,17 +543,24 @@ def cpu_model():
 
 
 def load_traffic(cfg_name, stripes):
-    """PMC-measured HBM bytes per launch (profiles/pmc_<cfg>.json, written by
-    tools/pmc_summary.py from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
-    bench at the config's default stripe count); None for other sizes."""
+    """PMC-measured HBM bytes per launch and where they come from: NOT
+    measured in this run, but read from profiles/pmc_<cfg>.json, written by
+    tools/pmc_summary.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes of this bench at the config's default stripe count (the file
+    names its round).  (None, reason) for other sizes or no file."""
     path = os.path.join(ROOT, "profiles", "pmc_%s.json" % cfg_name)
-    if not os.path.exists(path) or stripes != CONFIGS[cfg_name][4]:
-        return None
+    if not os.path.exists(path):
+        return None, "no PMC profile for this config"
+    if stripes != CONFIGS[cfg_name][4]:
+        return None, "PMC profile is for %d stripes, not %d" % (CONFIGS[cfg_name][4], stripes)
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+            j = json.load(f)
+    except Exception as exc:
+        return None, "unreadable PMC profile: %r" % exc
+    return j.get("hbm_bytes_per_launch"), ("profiles/pmc_%s.json (%s; rocprofv3 FETCH_SIZE + WRITE_SIZE passes, "
+                                          "gfx950-corrected; not measured in this run)"
+                                          % (cfg_name, j.get("round", "r02-final")))
 
 
 def launcher_cmd(argv, gpus, port, python=None):
@@ -417,8 +638,10 @@ EXTRA_CONFIGS = (("configs[3]", "rs8_small", None), ("configs[4]", "crs_enc", 32
 
 def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_ok):
     """One BASELINE config with its own warmup, the main line's barrier +
-    max-over-ranks timing, and a verified decode: the twin decode for
-    configs[4], a decode round trip of the first stripes for configs[3]."""
+    max-over-ranks timing, parity pins against the reference (sampled
+    encode stripes; codeword and non-codeword decode stripes) and a
+    verified decode: the timed twin decode for configs[4], an untimed
+    decode of the first stripes for configs[3]."""
     import torch
     from memec_amd import Codec, fill_random
     from memec_amd.shard import shard_range, timed_steps
@@ -444,10 +667,17 @@ def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_
                 "kernel_ms": round(kern, 4), "achieved_GBps": round(alg / (kern * 1e-3) / 1e9, 1),
                 "frac": round(alg / (kern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
+    def pin(rec):
+        rec["equal"] = all_ranks_ok(rec["equal"])
+        rec["ranks"] = world
+        return rec
+
     res = {"workload": workload_name(name, stripes, bool(strong_global), global_stripes),
            "scaling": "strong" if strong_global else "weak", "stripes_per_gpu": stripes,
            "global_stripes": global_stripes}
-    res.update(run(lambda: codec.encode(data, parity), (k + m) * cs * stripes))
+    enc_step = lambda: codec.encode(data, parity)  # noqa: E731
+    res.update(run(enc_step, (k + m) * cs * stripes))
+    res["parity"] = pin(check_encode(fam, k, m, cs, data, parity))
     twin = {"crs_enc": "crs_dec"}.get(name)
     erased = CONFIGS[twin][6] if twin else list(range(m))
     n = stripes if twin else min(stripes, 4096)
@@ -455,19 +685,35 @@ def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_
     st[:, :k] = data[:n]
     st[:, k:] = parity[:n]
     saved = st[:, erased].clone()
+    rec = plant_noncodewords(st, k, m, cs, 0x5EED + rank)
     st[:, erased] = 0
     present = sum(1 << i for i in range(k + m) if i not in erased)
+    dec_step = lambda: codec.decode(st, present)  # noqa: E731
     if twin:
-        dec = run(lambda: codec.decode(st, present), (k + len(erased)) * cs * n)
+        dec = run(dec_step, (k + len(erased)) * cs * n)
         dec["workload"] = workload_name(twin, n, True, global_stripes)
         dec["erased"] = erased
-        dec["verified"] = all_ranks_ok(torch.equal(st[:, erased], saved))
+    else:
+        dec_step()
+        torch.cuda.synchronize()
+    dpin = pin(check_decode(fam, k, m, cs, st, erased, rec))
+    restore_noncodewords(st, saved, erased, rec)
+    ok = all_ranks_ok(torch.equal(st[:, erased], saved))
+    if twin:
+        dec["parity"] = dpin
+        dec["verified"] = ok
         res["decode"] = dec
     else:
-        codec.decode(st, present)
-        torch.cuda.synchronize()
-        res["verified"] = all_ranks_ok(torch.equal(st[:, erased], saved))
-        res["verification"] = "decode of erasures %s restores the first %d encoded stripes" % (erased, n)
+        res["decode_parity"] = dpin
+        res["verified"] = ok
+        res["verification"] = ("decode of erasures %s restores the first %d encoded stripes (the %d planted "
+                               "non-codewords checked against the reference instead)" % (erased, n, len(rec["nc"])))
+    # the same launches with the arithmetic removed (byte-wise only): what
+    # this memory stream reaches without the GF(2^8) work, live on this box
+    tw = twin_rate(codec, enc_step, (k + m) * cs * stripes)
+    if tw:
+        res["xor_twin_GBps"] = round(tw, 1)
+        res["frac_of_xor_twin"] = round(res["achieved_GBps"] / tw, 4)
     del data, parity, st, saved
     codec.close()
     torch.cuda.empty_cache()
@@ -486,7 +732,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true",
                     help="encode configs: skip the decode twin measurement (configs[2] for configs[1])")
-    ap.add_argument("--no-ceiling", action="store_true", help="skip the on-box streaming-ceiling measurement (mec_xor)")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the live ceilings (the XOR twin of the timed launch, mec_xor)")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="default run: skip configs[3] and configs[4] beside the configs[1]/[2] line")
     ap.add_argument("--extra-configs", action="store_true",
@@ -605,7 +851,10 @@ def main():
         codewords_np = None  # CPU-baseline sample: GPU-encoded stripes before the erasure
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             threads_cb = args.cpu_threads or host_cores()[0]
-            codewords_np = stripe[:decode_sample(k, m, cs, threads_cb)].cpu().numpy()
+            codewords_np = stripe[:cpu_sample(k, m, cs, threads_cb)].cpu().numpy()
+        # random non-codewords planted in the second half pin the survivor
+        # choice against the reference (check_decode)
+        nc_rec = plant_noncodewords(stripe, k, m, cs, 0x5EED + rank)
         stripe[:, erased] = 0
 
         def step():
@@ -617,6 +866,46 @@ def main():
     ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     wall, kern_ms = timed_steps(step, args.steps, args.warmup, sync=torch.cuda.synchronize,
                                 dist=dist if use_pg else None, events=ev)  # one launch per step
+
+    def pin(rec):
+        rec["equal"] = all_ranks_ok(rec["equal"])
+        rec["ranks"] = world
+        return rec
+
+    # parity pins of the timed launches' outputs (before anything reuses them)
+    parity_pin, ok, gpu_parity_np = None, None, None
+    if op == "encode":
+        parity_pin = pin(check_encode(fam, k, m, cs, data, parity))
+        if rank == 0 and not args.no_cpu_baseline:
+            gpu_parity_np = parity[:64].cpu().numpy()
+    elif op == "decode":
+        parity_pin = pin(check_decode(fam, k, m, cs, stripe, erased, nc_rec))
+        if orig is not None:
+            restore_noncodewords(stripe, orig, erased, nc_rec)
+            ok = all_ranks_ok(torch.equal(stripe[:, erased], orig))
+    else:
+        # parity started as the parity of all-zero data and received the
+        # same delta n times: it must equal the encode of (delta in column
+        # j, zeros elsewhere) if n is odd, zero if n is even — checked on
+        # the GPU for 256 stripes, and against the reference's encode on
+        # stripes spread over the batch
+        import numpy as np
+        ref = torch.zeros(min(stripes, 256), m, cs, dtype=torch.uint8, device=dev)
+        if n_updates[0] % 2:
+            dz = torch.zeros(ref.shape[0], k, cs, dtype=torch.uint8, device=dev)
+            dz[:, j] = delta[:ref.shape[0]]
+            codec.encode(dz, ref)
+            del dz
+        ok = all_ranks_ok(torch.equal(parity[:ref.shape[0]], ref))
+        del ref
+        idx = spread(0, stripes, parity_count(k, m, cs))
+        dz = np.zeros((len(idx), k, cs), np.uint8)
+        if n_updates[0] % 2:
+            dz[:, j] = _rows(delta, idx)
+        want, vs = ref_encode(fam, k, m, cs, dz)
+        parity_pin = pin({"vs": vs, "stripes": len(idx), "equal": bool(np.array_equal(_rows(parity, idx), want)),
+                          "sample": "%d stripes spread over [0, %d): parity after %d delta updates vs the "
+                                    "reference's encode of the delta stripe" % (len(idx), stripes, n_updates[0])})
 
     # the metric is encode+decode: an encode config also times its decode
     # twin (configs[2] for configs[1]) on the just-encoded stripes, every
@@ -630,81 +919,65 @@ def main():
         st[:, k:] = parity
         dcodewords = None  # CPU-baseline sample of the twin: GPU-encoded codewords
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            dcodewords = st[:decode_sample(k, m, cs, args.cpu_threads or host_cores()[0])].cpu().numpy()
+            dcodewords = st[:cpu_sample(k, m, cs, args.cpu_threads or host_cores()[0])].cpu().numpy()
         saved = st[:, derased].clone()
+        drec = plant_noncodewords(st, k, m, cs, 0x5EED + 7 * rank + 1)
         st[:, derased] = 0
         dpresent = sum(1 << i for i in range(k + m) if i not in derased)
+        dstep = lambda: codec.decode(st, dpresent)  # noqa: E731
         dev_ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-        dwall, dkern = timed_steps(lambda: codec.decode(st, dpresent), args.steps, args.warmup,
+        dwall, dkern = timed_steps(dstep, args.steps, args.warmup,
                                    sync=torch.cuda.synchronize, dist=dist if use_pg else None, events=dev_ev)
         dalg = (k + len(derased)) * cs * stripes
+        dpin = pin(check_decode(fam, k, m, cs, st, derased, drec))
+        restore_noncodewords(st, saved, derased, drec)
         secondary = {"workload": workload_name(twin, stripes, args.strong, global_stripes), "erased": derased,
                      "value": round(global_stripes * k * cs * args.steps / dwall / 2**30, 3), "unit": "GiB/s",
                      "ms_per_step": round(dwall / args.steps * 1e3, 4), "kernel_ms": round(dkern, 4),
                      "achieved_GBps": round(dalg / (dkern * 1e-3) / 1e9, 1),
                      "frac": round(dalg / (dkern * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "parity": dpin,
                      "verified": all_ranks_ok(torch.equal(st[:, derased], saved))}
+        if not args.no_ceiling and rank == 0:
+            tw = twin_rate(codec, dstep, dalg)
+            if tw:
+                secondary["xor_twin_GBps"] = round(tw, 1)
+                secondary["frac_of_xor_twin"] = round(secondary["achieved_GBps"] / tw, 4)
         del st, saved
 
-    ceiling = None
+    # live ceilings, measured after every output above was checked: the
+    # arithmetic-free twin of the timed launch (mec_set_probe: same kernel,
+    # launch shape, loads and stores, every GF(2^8) product a plain XOR), and
+    # libmec's region XOR (Coding::bitwiseXOR, 2 reads + 1 write per lane)
+    # over 3 x 8 GiB, for reference
+    twin_gbps, xor_gbps = None, None
     if rank == 0 and not args.no_ceiling:
-        # on-box streaming ceiling: libmec's plain region XOR
-        # (Coding::bitwiseXOR; 2 non-temporal 16-B reads + 1 write per lane,
-        # no arithmetic to speak of) over 3 x 8 GiB, best of 15 launches
-        # over 5 occupancy caps — the same access shape as the coding kernels.  (torch's own copy kernel
-        # reaches only ~4.6-5.0 TB/s here, tools/ceil_probe.py.)
+        twin_gbps = twin_rate(codec, step, alg_bytes)
+        if op == "decode":
+            step()  # the outputs again (the twin overwrote them)
         from memec_amd import xor as mec_xor
         a = torch.empty(8 << 30, dtype=torch.uint8, device=dev)
         b = torch.empty_like(a)
         out = torch.empty_like(a)
         mec_xor(out, a, b)
         best = None
-        # the stream's own best occupancy: its default cap and a few others
-        # (MEC_WPC, memec_amd/csrc/stream_common.hpp)
-        saved = os.environ.pop("MEC_WPC", None)
-        for wpc in (None, "0", "12", "16", "24"):
-            if wpc is None:
-                os.environ.pop("MEC_WPC", None)
-            else:
-                os.environ["MEC_WPC"] = wpc
-            for _ in range(3):
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                mec_xor(out, a, b)
-                e1.record()
-                e1.synchronize()
-                ms = e0.elapsed_time(e1)
-                best = ms if best is None else min(best, ms)
-        os.environ.pop("MEC_WPC", None)
-        if saved is not None:
-            os.environ["MEC_WPC"] = saved
-        ceiling = 3 * a.numel() / (best * 1e-3) / 1e9
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            mec_xor(out, a, b)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        xor_gbps = 3 * a.numel() / (best * 1e-3) / 1e9
         del a, b, out
+        if op == "encode":
+            step()  # correct parity again for the e2e leg
 
     extras = None
     if args.config == "rs_enc" and not args.strong and not args.no_extra_configs and (args.extra_configs or not args.stripes):
         extras = {label: measure_extra(name, strong_global, args.steps, rank, world, dev, dist, all_ranks_ok)
                   for label, name, strong_global in EXTRA_CONFIGS}
-
-    ok = None
-    if op == "decode" and orig is not None:
-        ok = all_ranks_ok(torch.equal(stripe[:, erased], orig))
-    if op == "update":
-        # parity started as the parity of all-zero data and received the
-        # same delta n times: it must equal the encode of (delta in column
-        # j, zeros elsewhere) if n is odd, zero if n is even
-        ref = torch.zeros(min(stripes, 256), m, cs, dtype=torch.uint8, device=dev)
-        if n_updates[0] % 2:
-            dz = torch.zeros(ref.shape[0], k, cs, dtype=torch.uint8, device=dev)
-            dz[:, j] = delta[:ref.shape[0]]
-            codec.encode(dz, ref)
-            del dz
-        ok = all_ranks_ok(torch.equal(parity[:ref.shape[0]], ref))
-        del ref
-
-    gpu_parity_np = None
-    if rank == 0 and op == "encode" and not args.no_cpu_baseline:
-        gpu_parity_np = parity[:64].cpu().numpy()
 
     e2e = None
     if args.e2e and rank == 0 and op == "encode":
@@ -735,6 +1008,7 @@ def main():
                **res}
 
     if rank == 0:
+        traffic, traffic_src = load_traffic(args.config, stripes)
         # data GiB/s: k data chunks per stripe (encode / decode), the one
         # delta chunk per stripe for updates
         value = global_stripes * (cs if op == "update" else k * cs) * args.steps / wall / 2**30
@@ -756,10 +1030,16 @@ def main():
                        "chunk_bytes": cs, "stripes_per_gpu": stripes, "global_stripes": global_stripes,
                        "op": op, "erased": erased, "parallelism": "stripe-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(args.config, stripes),
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4),
-                         "stream_ceiling_GBps": round(ceiling, 1) if ceiling else None,
-                         "frac_of_stream_ceiling": round(achieved / ceiling, 4) if ceiling else None},
+                         "xor_twin_GBps": round(twin_gbps, 1) if twin_gbps else None,
+                         "frac_of_xor_twin": round(achieved / twin_gbps, 4) if twin_gbps else None,
+                         "region_xor_2r1w_GBps": round(xor_gbps, 1) if xor_gbps else None,
+                         "ceilings": "xor_twin = this launch with every GF(2^8) product a plain XOR "
+                                     "(mec_set_probe), live, best of 5; region_xor_2r1w = mec_xor over "
+                                     "3 x 8 GiB, live, best of 5"},
+            "parity": parity_pin,
             "cpu_baseline": None,
         }
         if ok is not None:
@@ -772,8 +1052,6 @@ def main():
             line["other_configs"] = extras
         if secondary:
             line["decode"] = secondary
-            if ceiling:
-                secondary["frac_of_stream_ceiling"] = round(secondary["achieved_GBps"] / ceiling, 4)
         if not args.no_cpu_baseline and world == 1:
             threads, host = host_cores()
             threads = args.cpu_threads or threads

@@ -79,7 +79,7 @@
 extern "C" {
 #endif
 
-#define MEC_ABI_VERSION 3
+#define MEC_ABI_VERSION 4
 #define MEC_MAX_CHUNKS 32 /* k + m <= 32: RS_N_MAX / CRS_N_MAX (rscoding.hh:5, cauchycoding.hh:5) */
 
 typedef enum {
@@ -293,6 +293,29 @@ int mec_set_coalescing(mec_ctx *ctx, uint32_t max_batch);
  * workers call the CPU plugin directly (worker.cc:128-137). */
 int mec_set_host_queue(mec_ctx *ctx, uint32_t slots);
 int mec_get_stats(const mec_ctx *ctx, mec_stats *out);
+
+/* ---- measurement and experiments (no reference counterpart) --------------- */
+
+#define MEC_PROBE_OFF 0
+#define MEC_PROBE_XOR 1
+/* MEC_PROBE_XOR: this context's strided byte-wise launches (mec_encode,
+ * mec_decode, mec_decode_split, mec_encode_update, and the single-stripe
+ * host calls' launches) run their arithmetic-free
+ * twin — the same kernel, launch shape, loads and stores with every GF(2^8)
+ * product replaced by a plain XOR — so a bench can measure, live, the rate
+ * the same memory stream reaches without the coding arithmetic.  The
+ * outputs are NOT codes while it is on.  MEC_PROBE_OFF (default) restores
+ * normal coding.  MEC_EINVAL for MEC_CAUCHY_GOOD. */
+int mec_set_probe(mec_ctx *ctx, int mode);
+
+/* Launch-shape experiment overrides.  libmec reads MEC_SGROUP, MEC_WINDOWS,
+ * MEC_BLOCK, MEC_GBLOCK, MEC_GWPC, MEC_BM_VW, MEC_WPC and MEC_COPY_THREADS
+ * from the environment once, at first use, never on a launch path; this
+ * call changes one at run time (same name and value syntax as the
+ * variable; value NULL = unset, i.e. the built-in rule).  Changes are
+ * atomic: a launch running concurrently sees the old or the new value.
+ * MEC_EINVAL for an unknown name. */
+int mec_set_knob(const char *name, const char *value);
 
 #ifdef __cplusplus
 }

@@ -7,7 +7,7 @@ Layers:
   memec_amd/csrc/coding/   C++ drop-in for class Coding (libmemec_coding.so)
   memec_amd.codec          Python binding of the C ABI (tests, bench)
 """
-from ._lib import FAMILIES, MecError, lib  # noqa: F401
+from ._lib import FAMILIES, MecError, lib, set_knob  # noqa: F401
 from .codec import Codec, fill_random, host_register, host_unregister, xor  # noqa: F401
 
-__all__ = ["Codec", "MecError", "FAMILIES", "fill_random", "xor", "host_register", "host_unregister", "lib"]
+__all__ = ["Codec", "MecError", "FAMILIES", "fill_random", "xor", "host_register", "host_unregister", "lib", "set_knob"]

@@ -20,6 +20,7 @@ SYMBOLS = (
     "mec_encode_update", "mec_xor", "mec_fill_random", "mec_encode_host", "mec_decode_host",
     "mec_encode_update_host", "mec_encode_host_batch", "mec_host_register", "mec_host_unregister",
     "mec_encode_batch", "mec_decode_batch", "mec_encode_update_batch", "mec_set_coalescing", "mec_set_host_queue", "mec_get_stats",
+    "mec_set_probe", "mec_set_knob",
 )
 MEM_DEVICE, MEM_HOST = 0, 1
 
@@ -88,8 +89,17 @@ def lib():
     L.mec_set_coalescing.argtypes = [vp, u32]
     L.mec_set_host_queue.argtypes = [vp, u32]
     L.mec_get_stats.argtypes = [vp, ctypes.POINTER(MecStats)]
+    L.mec_set_probe.argtypes = [vp, ctypes.c_int]
+    L.mec_set_knob.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     _lib = L
     return L
+
+
+def set_knob(name, value):
+    """Change a launch-shape experiment knob at run time (mec_set_knob):
+    name = the environment variable's name, value = its string syntax, None =
+    back to the built-in rule."""
+    check(lib().mec_set_knob(name.encode(), None if value is None else str(value).encode()))
 
 
 def check(rc):

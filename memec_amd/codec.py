@@ -198,6 +198,12 @@ class Codec:
         registered host memory (mec_set_host_queue); 0 stops it."""
         check(lib().mec_set_host_queue(self._h, slots))
 
+    def set_probe(self, on):
+        """Measurement only (mec_set_probe): while on, this context's strided
+        byte-wise launches run their arithmetic-free XOR twin (outputs are
+        not codes)."""
+        check(lib().mec_set_probe(self._h, 1 if on else 0))
+
     def stats(self):
         st = _lib.MecStats()
         check(lib().mec_get_stats(self._h, ctypes.byref(st)))

@@ -20,6 +20,7 @@
 #include <thread>
 
 #include "ctx.hpp"
+#include "knobs.hpp"
 
 namespace mec {
 namespace core {
@@ -403,9 +404,9 @@ struct Copy {
 
 // Threads for packing / unpacking staged chunks (MEC_COPY_THREADS, default 8).
 unsigned copy_threads() {
-    const char *e = std::getenv("MEC_COPY_THREADS");
-    const int v = e ? std::atoi(e) : 8;
-    return unsigned(std::max(1, std::min(v, 64)));
+    const int64_t e = detail::knob(detail::kKnobCopyThreads);
+    const int64_t v = e != detail::kKnobUnset ? e : 8;
+    return unsigned(std::max<int64_t>(1, std::min<int64_t>(v, 64)));
 }
 
 // memcpy of many equal-sized chunks, split over a few threads when large.

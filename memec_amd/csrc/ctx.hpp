@@ -168,6 +168,9 @@ struct mec_ctx {
     // multi-GPU context (multi.cpp): one ordinary context per device
     std::vector<mec_ctx *> shards;
     std::atomic<uint32_t> rr{0};
+    // mec_set_probe: MEC_PROBE_XOR runs strided byte-wise launches as their
+    // arithmetic-free twin (measurement only)
+    std::atomic<int> probe{0};
 
     bool byte_wise() const { return family != MEC_CAUCHY_GOOD; }
     mec::Scheme scheme() const {

@@ -66,8 +66,12 @@ __device__ __forceinline__ u32x4 xor3(const u32x4 &a, const u32x4 &b, const u32x
 //               distribution rows, reed_sol.c:269-297, and ISA-L's
 //               gf_gen_rs_matrix parity rows, ec_base.c:62-79): those
 //               entries are plain XORs, the rest through tables.
+//   kGf8Xor   — measurement twin (mec_set_probe): every product replaced by
+//               a plain XOR, same loads, stores and launch shape; the
+//               outputs are not codes.
 constexpr int kGf8Dense = 0;
 constexpr int kGf8Vand = 1;
+constexpr int kGf8Xor = 2;
 
 // acc[i] ^= sum_j coef(i, j) * d[j] for one 16-byte unit.  TB = the LDS
 // permute tables (8 dwords per coefficient b = i*K + j: t0 t1 u0 u1 v).
@@ -78,6 +82,15 @@ constexpr int kGf8Vand = 1;
 // costs 3 v_perm + 1.5 v_bitop3 per dword and a unit one 0.5 v_bitop3.
 template <int K, int R, int S>
 __device__ __forceinline__ void gf8_apply(const u32x4 (&d)[K], u32x4 (&acc)[R], const uint32_t *tb) {
+    if constexpr (S == kGf8Xor) {
+        u32x4 x = d[0];
+#pragma unroll
+        for (int j = 1; j + 1 < K; j += 2) x = xor3(x, d[j], d[j + 1]);
+        if constexpr (K % 2 == 0) x ^= d[K - 1];
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[i] ^= x;
+        return;
+    }
     u32x4 pend[R];
     bool has[R];
 #pragma unroll
@@ -266,7 +279,12 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                 p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
                 const dim3 grid(ns * g.tiles), block(bt);
                 const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, p.win > 1, !vand, L.accumulate));
-                if (bt == kWaveBlock) {
+                if (L.probe) {
+                    if (bt == kWaveBlock)
+                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Xor, kWaveBlock>), grid, block, lds, stream, p);
+                    else
+                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Xor, kThreads>), grid, block, lds, stream, p);
+                } else if (bt == kWaveBlock) {
                     if (vand)
                         hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand, kWaveBlock>), grid, block, lds, stream, p);
                     else

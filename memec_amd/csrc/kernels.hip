@@ -26,6 +26,7 @@
 
 #include "gf_math.hpp"
 #include "kernels.hpp"
+#include "knobs.hpp"
 #include "bm_kernel.hpp"
 #include "gf8_kernel.hpp"
 #include "gather_kernel.hpp"
@@ -220,7 +221,7 @@ using namespace detail;
 namespace detail {
 uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool in_place, bool bitmatrix,
                       uint32_t &run) {
-    const char *e = std::getenv("MEC_SGROUP");  // read per launch: experiments flip it
+    const int64_t kg = knob(kKnobSgroup), kr = knob(kKnobSrun);  // experiments (mec_set_knob)
     run = 8;
     // chunks of 2 MiB or more: 16 stripes, runs of 8 tiles
     // (tools/sgroup_ab.py, profiles/r02/sgroup/; RS(10,4) split encode 2 MiB
@@ -232,18 +233,17 @@ uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool i
     // 68.7 with the same map (profiles/r02/sgroup/sgroup_ab_crs.log)
     (void)in_place;
     uint32_t g = (!bitmatrix && chunk >= (uint64_t(2) << 20)) ? 16u : 0u;
-    if (e) {
-        if (e[0] == 'x') return tiles % 8 == 0 ? kXcdRegions : 0u;
-        g = uint32_t(std::atoi(e));
-        if (const char *c = std::strchr(e, ':')) run = uint32_t(std::atoi(c + 1));
+    if (kg != kKnobUnset) {
+        if (kg == kKnobXcd) return tiles % 8 == 0 ? kXcdRegions : 0u;
+        g = uint32_t(std::max<int64_t>(kg, 0));
+        if (kr != kKnobUnset) run = uint32_t(std::max<int64_t>(kr, 0));
     }
     if (g <= 1 || run == 0 || run % 8 != 0 || tiles % run != 0 || n_stripes < 2) return 0;
     return std::min(g, n_stripes);
 }
 
 uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span) {
-    const char *e = std::getenv("MEC_WINDOWS");  // read per launch: experiments flip it
-    const int forced = e ? std::atoi(e) : 0;
+    const int64_t forced = knob(kKnobWindows);  // experiments (mec_set_knob)
     if (forced > 0) return uint32_t(forced);
     const int64_t a0 = int64_t(reinterpret_cast<uintptr_t>(src)), b0 = int64_t(reinterpret_cast<uintptr_t>(dst));
     const int64_t a1 = a0 + std::max<int64_t>(src_span, 0), b1 = b0 + std::max<int64_t>(dst_span, 0);
@@ -252,15 +252,14 @@ uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int6
 uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place) {
     // gathered (pointer-table) launches are instantiated for kThreads only
     if (!strided) return uint32_t(kThreads);
-    const char *e = std::getenv("MEC_BLOCK");  // read per launch: experiments flip it
-    const int forced = e ? std::atoi(e) : 0;
+    const int64_t forced = knob(kKnobBlock);  // experiments (mec_set_knob)
     if (forced == kWaveBlock || forced == kThreads) return uint32_t(forced);
     if (win == 1) return uint32_t(kWaveBlock);
     return wave_in_place ? uint32_t(kWaveBlock) : uint32_t(kThreads);
 }
 uint32_t gathered_block_threads(uint8_t gshape) {
-    const char *e = std::getenv("MEC_GBLOCK");  // read per launch: experiments flip it
-    if (e) return std::atoi(e) == kWaveBlock ? uint32_t(kWaveBlock) : uint32_t(kThreads);
+    const int64_t e = knob(kKnobGblock);  // experiments (mec_set_knob)
+    if (e != kKnobUnset) return e == kWaveBlock ? uint32_t(kWaveBlock) : uint32_t(kThreads);
     return gshape == 1 ? uint32_t(kWaveBlock) : uint32_t(kThreads);
 }
 namespace {
@@ -276,8 +275,8 @@ uint32_t lds_for_waves(uint32_t per, uint32_t static_lds, uint32_t waves) {
 }  // namespace
 
 uint32_t gathered_lds(uint32_t bt, uint32_t static_lds, uint8_t gshape) {
-    const char *e = std::getenv("MEC_GWPC");  // read per launch: experiments flip it
-    const int w = e ? std::atoi(e) : (gshape == 1 ? 16 : gshape == 2 ? 12 : 0);
+    const int64_t e = knob(kKnobGwpc);  // experiments (mec_set_knob)
+    const int64_t w = e != kKnobUnset ? e : (gshape == 1 ? 16 : gshape == 2 ? 12 : 0);
     if (w <= 0) return 0;
     return lds_for_waves(std::max<uint32_t>(1, bt / 64), static_lds, uint32_t(w));
 }
@@ -307,8 +306,8 @@ uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accum
 
 uint32_t bm_lane_bytes(int w, int rows, uint64_t chunk, bool in_place) {
     if (w > 4) return 8;
-    const char *e = std::getenv("MEC_BM_VW");  // read per launch: experiments flip it
-    if (e) return std::atoi(e) == 2 ? 8 : 16;
+    const int64_t e = knob(kKnobBmVw);  // experiments (mec_set_knob)
+    if (e != kKnobUnset) return e == 2 ? 8 : 16;
     if (!in_place) return 8;
     return (chunk <= (8u << 10) || (rows <= 2 && chunk <= (32u << 10))) ? 8 : 16;
 }
@@ -321,12 +320,13 @@ uint32_t bm_target_waves(int rows, int w, int vw, bool in_place) {
 }
 
 uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32_t waves) {
-    const char *e = std::getenv("MEC_WPC");  // read per launch: experiments flip it
-    if (e) waves = uint32_t(std::max(0, std::atoi(e)));
+    const int64_t e = knob(kKnobWpc);  // experiments (mec_set_knob)
+    const bool forced = e != kKnobUnset;
+    if (forced) waves = uint32_t(std::max<int64_t>(0, e));
     // a block with less than one wave's worth of units streams too little
     // per wave for a cap to pay (CRS at 2 KiB chunks: 75 % uncapped, 51 %
     // capped, profiles/r02/sweep)
-    if (waves == 0 || (!e && active < 64)) return 0;
+    if (waves == 0 || (!forced && active < 64)) return 0;
     const uint32_t act = std::min(bt, std::max<uint32_t>(active, 1));
     return lds_for_waves(std::max<uint32_t>(1, (act + 63) / 64), static_lds, waves);
 }

@@ -41,6 +41,9 @@ struct Gf8Launch {
     // aligned, 2 = some are not (MemEC's 8-byte ChunkPool headers); 0 =
     // unknown / host memory (gathered_block_threads)
     uint8_t gshape;
+    // measurement twin (mec_set_probe): strided launches run the same
+    // kernel with every product a plain XOR (kGf8Xor); outputs are not codes
+    bool probe;
     Gf8Coef coef[kMaxRows][kMaxSrc];
 };
 

@@ -1,0 +1,66 @@
+// knobs.cpp — experiment overrides, read from the environment once (see
+// knobs.hpp).
+#include "knobs.hpp"
+
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+
+namespace mec {
+namespace detail {
+namespace {
+
+struct Knobs {
+    std::atomic<int64_t> v[kKnobCount];
+    Knobs() {
+        for (auto &x : v) x.store(kKnobUnset, std::memory_order_relaxed);
+        for (const char *n : {"MEC_SGROUP", "MEC_WINDOWS", "MEC_BLOCK", "MEC_GBLOCK", "MEC_GWPC", "MEC_BM_VW",
+                              "MEC_WPC", "MEC_COPY_THREADS"})
+            apply(n, std::getenv(n));
+    }
+    bool apply(const char *name, const char *value) {
+        auto put = [&](Knob k, int64_t x) { v[k].store(x, std::memory_order_relaxed); };
+        const bool unset = value == nullptr;
+        const int64_t num = unset ? kKnobUnset : int64_t(std::atoll(value));
+        if (!std::strcmp(name, "MEC_SGROUP")) {
+            if (unset) {
+                put(kKnobSgroup, kKnobUnset);
+                put(kKnobSrun, kKnobUnset);
+            } else if (value[0] == 'x') {
+                put(kKnobSgroup, kKnobXcd);
+                put(kKnobSrun, kKnobUnset);
+            } else {
+                put(kKnobSgroup, num);
+                const char *c = std::strchr(value, ':');
+                put(kKnobSrun, c ? int64_t(std::atoll(c + 1)) : kKnobUnset);
+            }
+            return true;
+        }
+        static const struct {
+            const char *name;
+            Knob k;
+        } kPlain[] = {{"MEC_WINDOWS", kKnobWindows}, {"MEC_BLOCK", kKnobBlock},   {"MEC_GBLOCK", kKnobGblock},
+                      {"MEC_GWPC", kKnobGwpc},       {"MEC_BM_VW", kKnobBmVw},     {"MEC_WPC", kKnobWpc},
+                      {"MEC_COPY_THREADS", kKnobCopyThreads}};
+        for (const auto &p : kPlain)
+            if (!std::strcmp(name, p.name)) {
+                put(p.k, num);
+                return true;
+            }
+        return false;
+    }
+};
+
+Knobs &knobs() {
+    static Knobs k;
+    return k;
+}
+
+}  // namespace
+
+int64_t knob(Knob k) { return knobs().v[k].load(std::memory_order_relaxed); }
+
+bool set_knob(const char *name, const char *value) { return name && knobs().apply(name, value); }
+
+}  // namespace detail
+}  // namespace mec

@@ -1,0 +1,37 @@
+// knobs.hpp — launch-shape experiment overrides.
+//
+// Each knob is read from its environment variable ONCE (first use, a C++11
+// thread-safe static) and held in an atomic; mec_set_knob() changes it at
+// run time.  No launch path calls getenv, so the library never races a
+// caller's setenv/putenv, and an experiment flips a knob between launches
+// through the API instead of the environment.
+#pragma once
+
+#include <cstdint>
+
+namespace mec {
+namespace detail {
+
+enum Knob : int {
+    kKnobSgroup = 0,  // MEC_SGROUP=<group>[:<run>] | x  (group; kKnobXcd for "x")
+    kKnobSrun,        //   ... its run length
+    kKnobWindows,     // MEC_WINDOWS=<n>
+    kKnobBlock,       // MEC_BLOCK=64|256
+    kKnobGblock,      // MEC_GBLOCK=64|256
+    kKnobGwpc,        // MEC_GWPC=<waves> (0 = no cap)
+    kKnobBmVw,        // MEC_BM_VW=2|4
+    kKnobWpc,         // MEC_WPC=<waves> (0 = no cap)
+    kKnobCopyThreads, // MEC_COPY_THREADS=<n>
+    kKnobCount
+};
+constexpr int64_t kKnobUnset = INT64_MIN;
+constexpr int64_t kKnobXcd = -2;  // MEC_SGROUP=x
+
+// Current value, or kKnobUnset.
+int64_t knob(Knob k);
+// name: the environment variable's name ("MEC_WPC", ...); value: the same
+// syntax as the variable, NULL = unset.  Returns false for an unknown name.
+bool set_knob(const char *name, const char *value);
+
+}  // namespace detail
+}  // namespace mec

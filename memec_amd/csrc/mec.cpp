@@ -3,6 +3,7 @@
 // staging.  Pointer-table batches, the host pipeline and the request
 // coalescer live in batch.cpp.
 #include "ctx.hpp"
+#include "knobs.hpp"
 
 #include <chrono>
 #include <cstdarg>
@@ -68,6 +69,7 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
             L.len = c->cs;
             L.n_stripes = n_stripes;
             L.accumulate = accumulate;
+            L.probe = c->probe.load(std::memory_order_relaxed) == MEC_PROBE_XOR;
             for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
             for (int i = 0; i < rows; ++i) L.dst_off[i] = lay.dst_off[r0 + i];
             for (int i = 0; i < rows; ++i)
@@ -437,6 +439,21 @@ int mec_encode_update(mec_ctx *c, uint32_t data_index, const uint8_t *delta, int
 int mec_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, void *stream) {
     if ((!dst || !a || !b) && len) return fail(MEC_EINVAL, "null buffer");
     HIP_TRY(mec::launch_xor(dst, a, b, len, hipStream_t(stream)));
+    return MEC_OK;
+}
+
+int mec_set_probe(mec_ctx *c, int mode) {
+    if (!c) return fail(MEC_EINVAL, "null context");
+    if (mode != MEC_PROBE_OFF && mode != MEC_PROBE_XOR) return fail(MEC_EINVAL, "unknown probe mode %d", mode);
+    if (mode == MEC_PROBE_XOR && !c->byte_wise())
+        return fail(MEC_EINVAL, "the XOR twin exists for byte-wise families only");
+    c->probe.store(mode, std::memory_order_relaxed);
+    return MEC_OK;
+}
+
+int mec_set_knob(const char *name, const char *value) {
+    if (!name) return fail(MEC_EINVAL, "null knob name");
+    if (!mec::detail::set_knob(name, value)) return fail(MEC_EINVAL, "unknown knob %s", name);
     return MEC_OK;
 }
 

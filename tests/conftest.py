@@ -24,3 +24,19 @@ def pytest_collection_modifyitems(config, items):
 def golden():
     import _oracle
     return _oracle.golden()
+
+
+@pytest.fixture
+def knobs():
+    """Set libmec launch-shape knobs through mec_set_knob (the library reads
+    the environment once; experiments change knobs through the API) and put
+    every touched knob back to its built-in rule afterwards."""
+    import memec_amd
+    touched = set()
+
+    def set_(name, value):
+        touched.add(name)
+        memec_amd.set_knob(name, value)
+    yield set_
+    for name in touched:
+        memec_amd.set_knob(name, None)

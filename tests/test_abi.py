@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(_lib.SYMBOLS)
-    assert L.mec_abi_version() == 3
+    assert L.mec_abi_version() == 4
 
 
 def test_coding_adapter_library_links():
@@ -149,3 +149,24 @@ def test_gf8_perm_decomposition_emulated():
             got = perm(t1, t0, s0) ^ perm(u1, u0, s1) ^ perm(v, v, s2)
             want = sum(int(mul[c][(x >> (8 * i)) & 0xFF]) << (8 * i) for i in range(4))
             assert got == want, (c, x)
+
+
+def test_knobs_through_the_api_not_the_environment():
+    """Launch-shape knobs are read from the environment once; mec_set_knob
+    changes them at run time (no getenv on a launch path) and refuses
+    unknown names."""
+    import memec_amd
+    for name, value in (("MEC_WPC", "12"), ("MEC_SGROUP", "x"), ("MEC_SGROUP", "16:8"), ("MEC_BLOCK", "256"),
+                        ("MEC_BM_VW", "2"), ("MEC_GBLOCK", "64"), ("MEC_GWPC", "0"), ("MEC_WINDOWS", "2"),
+                        ("MEC_COPY_THREADS", "4")):
+        memec_amd.set_knob(name, value)
+        memec_amd.set_knob(name, None)
+    with pytest.raises(MecError):
+        memec_amd.set_knob("MEC_NO_SUCH_KNOB", "1")
+    src = open(os.path.join(ROOT, "memec_amd", "csrc", "kernels.hip")).read()
+    assert "getenv" not in src
+
+
+def test_probe_needs_a_context():
+    L = _lib.lib()
+    assert L.mec_set_probe(None, 1) == _lib.MEC_EINVAL

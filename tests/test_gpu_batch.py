@@ -361,11 +361,11 @@ def test_update_batch_single_column(fam):
 
 
 @pytest.mark.parametrize("block", ["64", "256"])
-def test_block_override_every_launch_kind(block, monkeypatch):
+def test_block_override_every_launch_kind(block, knobs):
     """MEC_BLOCK (layout experiments) forces the block size of strided
     launches and must leave results unchanged; gathered (pointer-table)
     launches ignore it (their kernels exist for 256 threads only)."""
-    monkeypatch.setenv("MEC_BLOCK", block)
+    knobs("MEC_BLOCK", block)
     test_encode_batch_scattered("rs", "device", 8)
     test_encode_batch_scattered("cauchy", "device", 8)
     for fam in ("rs", "cauchy"):

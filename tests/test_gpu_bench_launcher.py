@@ -20,7 +20,7 @@ def _run(*extra):
         env.pop(v, None)
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
                           "--warmup", "1", "--no-ceiling", *extra],
-                         env=env, capture_output=True, text=True, timeout=300)
+                         env=env, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout
@@ -35,6 +35,25 @@ def test_bench_gpus2_spawns_ranks_weak():
     assert rec["decode"]["verified"] is True
     assert rec["value"] > 0 and rec["roofline"]["kernel_ms"] > 0
     assert rec["cpu_baseline"] is None  # rank 0 at N=1 only
+
+
+@pytest.mark.timeout(500)
+def test_bench_gpus2_default_line_rehearsal():
+    """The driver's default 8-GPU line at N=2: configs[1]/[2] on 64 stripes
+    per rank plus other_configs — configs[3] per rank and the 32768-stripe
+    configs[4] batch split 16384 / 16384 — every output verified and
+    parity-pinned against the reference on both ranks."""
+    rec = _run("--stripes", "64", "--extra-configs")
+    assert rec["n_gpus"] == 2 and rec["dist"]["world_size"] == 2
+    assert rec["parity"]["equal"] is True and rec["parity"]["ranks"] == 2
+    assert rec["decode"]["verified"] is True and rec["decode"]["parity"]["equal"] is True
+    assert rec["decode"]["parity"]["non_codeword_stripes"] > 0
+    c3, c4 = rec["other_configs"]["configs[3]"], rec["other_configs"]["configs[4]"]
+    assert c3["stripes_per_gpu"] == 65536 and c3["global_stripes"] == 131072
+    assert c3["verified"] is True and c3["parity"]["equal"] is True and c3["decode_parity"]["equal"] is True
+    assert c4["scaling"] == "strong" and c4["stripes_per_gpu"] == 16384 and c4["global_stripes"] == 32768
+    assert c4["parity"]["equal"] is True
+    assert c4["decode"]["verified"] is True and c4["decode"]["parity"]["equal"] is True
 
 
 def test_bench_gpus2_strong_crs():

@@ -74,23 +74,23 @@ def _check_all_layouts(fam, cs, seed):
 
 @pytest.mark.parametrize("cs", [96, 4096, 4128, 65536])
 @pytest.mark.parametrize("vw", ["2", "4", None])
-def test_bitmatrix_lane_widths(vw, cs, monkeypatch):
+def test_bitmatrix_lane_widths(vw, cs, knobs):
     """8- and 16-byte lane slices (MEC_BM_VW), and the rule's own choice:
     packets of 24 B and 1032 B leave tails for 16-byte slices only."""
     if vw is None:
-        monkeypatch.delenv("MEC_BM_VW", raising=False)
+        knobs("MEC_BM_VW", None)
     else:
-        monkeypatch.setenv("MEC_BM_VW", vw)
+        knobs("MEC_BM_VW", vw)
     _check_all_layouts("cauchy", cs, 900 + cs % 997)
 
 
 @pytest.mark.parametrize("fam", ["rs", "cauchy", "isal_rs"])
 @pytest.mark.parametrize("block,wpc", [("64", "0"), ("64", "6"), ("256", "24"), ("256", "0")])
-def test_block_and_wave_cap_overrides(fam, block, wpc, monkeypatch):
+def test_block_and_wave_cap_overrides(fam, block, wpc, knobs):
     """Forced block sizes and resident-wave caps (down to one block per CU's
     share of LDS) change timing only."""
-    monkeypatch.setenv("MEC_BLOCK", block)
-    monkeypatch.setenv("MEC_WPC", wpc)
+    knobs("MEC_BLOCK", block)
+    knobs("MEC_WPC", wpc)
     _check_all_layouts(fam, 8192, 1300)
 
 
@@ -139,29 +139,29 @@ def _stripes_km(fam, k, m, cs, n, seed):
 
 
 @pytest.mark.parametrize("group", ["0", "3:8", "7:16", "4:64", "64:8", "bad:7"])
-def test_stripe_group_overrides(group, monkeypatch):
+def test_stripe_group_overrides(group, knobs):
     """The stripe-group block map (stream_common.hpp stripe_tile) with
     forced groups and run lengths, a last group shorter than the rest
     (N = 20 stripes), and an invalid run (falls back to the identity map):
     every layout stays bit-exact.  64 KiB chunks: 64 one-wave tiles."""
-    monkeypatch.setenv("MEC_SGROUP", group)
+    knobs("MEC_SGROUP", group)
     _check_all_layouts("rs", 65536, 1500)
 
 
-def test_stripe_groups_default_rule_large_chunks(monkeypatch):
+def test_stripe_groups_default_rule_large_chunks(knobs):
     """Split-layout encodes with chunks of 2 MiB or more take the grouped
     map by default (16 stripes, runs of 8 tiles): RS(4,2) at 2 MiB over 19
     stripes (one full group and a short one) equals the identity map, and
     its first and last stripes equal the oracle."""
     k, m, cs, n = 4, 2, 2 << 20, 19
-    monkeypatch.delenv("MEC_SGROUP", raising=False)
+    knobs("MEC_SGROUP", None)
     c = Codec("rs", k, m, cs)
     data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
     from memec_amd import fill_random
     fill_random(data, 4242)
     par = torch.zeros(n, m, cs, dtype=torch.uint8, device="cuda")
     c.encode(data, par)
-    monkeypatch.setenv("MEC_SGROUP", "0")
+    knobs("MEC_SGROUP", "0")
     ref = torch.zeros_like(par)
     c.encode(data, ref)
     torch.cuda.synchronize()

@@ -362,6 +362,61 @@ def test_xor():
     assert np.array_equal(to_np(a), O.fill(5000, 3) ^ O.fill(5000, 4))
 
 
+@pytest.mark.parametrize("k,m,cs,layout", [(10, 4, 65536, "split"), (4, 2, 4096, "inplace"), (3, 1, 4096 + 16, "split")])
+def test_xor_twin_probe(k, m, cs, layout):
+    """mec_set_probe(MEC_PROBE_XOR): the same launches with every product a
+    plain XOR (the bench's live ceiling) — each output is the XOR of the
+    launch's sources; switching it off codes again, bit-exact."""
+    n = 5
+    c = Codec("rs", k, m, cs)
+    data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
+    from memec_amd import fill_random
+    fill_random(data, 31 + k)
+    host = data.cpu().numpy()
+    x = np.bitwise_xor.reduce(host, axis=1)
+    if layout == "split":
+        par = torch.zeros(n, m, cs, dtype=torch.uint8, device="cuda")
+        c.set_probe(True)
+        c.encode(data, par)
+        c.set_probe(False)
+        torch.cuda.synchronize()
+        got = par.cpu().numpy()
+        full = cs // 16 * 16  # the < 16-byte tail is always coded (tail kernel)
+        for i in range(m):
+            assert np.array_equal(got[:, i, :full], x[:, :full])
+        c.encode(data, par)
+        torch.cuda.synchronize()
+        got = par.cpu().numpy()
+        for s_ in (0, n - 1):
+            assert np.array_equal(got[s_], np.stack(O.encode("rs", k, m, [host[s_, j].copy() for j in range(k)], cs)))
+    else:
+        st = torch.zeros(n, k + m, cs, dtype=torch.uint8, device="cuda")
+        st[:, :k] = data
+        c.encode(st[:, :k], st[:, k:])
+        want = st.clone()
+        st[:, [0, 1]] = 0
+        present = sum(1 << i for i in range(2, k + m))
+        c.set_probe(True)
+        c.decode(st, present)
+        torch.cuda.synchronize()
+        sv = want.cpu().numpy()[:, 2:2 + k]  # the decode plan reads the first k survivors
+        xs = np.bitwise_xor.reduce(sv, axis=1)
+        got = st.cpu().numpy()
+        assert np.array_equal(got[:, 0], xs) and np.array_equal(got[:, 1], xs)
+        c.set_probe(False)
+        c.decode(st, present)
+        torch.cuda.synchronize()
+        assert torch.equal(st, want)
+    c.close()
+
+
+def test_xor_twin_probe_refuses_bitmatrix():
+    c = Codec("cauchy", 4, 2, 4096)
+    with pytest.raises(MecError):
+        c.set_probe(True)
+    c.close()
+
+
 def test_xor_grid_stride_past_16_gib():
     """Past 2^24 one-wave tiles (16 GiB) the launch strides its grid; the
     tail tile is partial too."""

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import Codec, fill_random, set_knob  # noqa: E402
 
 CASES = [("rs", 4, 2, [0, 1]), ("rs", 10, 4, [0, 1, 2, 3]), ("cauchy", 12, 4, [0, 1, 2, 3])]
 SIZES = [4096, 16384, 65536, 262144, 1 << 20]
@@ -49,7 +49,7 @@ def main():
             res = {64: [], 256: []}
             for _ in range(5):
                 for b in (64, 256):
-                    os.environ["MEC_BLOCK"] = str(b)
+                    set_knob("MEC_BLOCK", str(b))
                     step()
                     ev[0].record()
                     for _ in range(10):
@@ -57,7 +57,7 @@ def main():
                     ev[1].record()
                     ev[1].synchronize()
                     res[b].append(ev[0].elapsed_time(ev[1]) / 10)
-            os.environ.pop("MEC_BLOCK", None)
+            set_knob("MEC_BLOCK", None)
             line = "%s(%d,%d) cs=%7d n=%6d" % (fam, k, m, cs, n)
             for b in (64, 256):
                 med = statistics.median(res[b])

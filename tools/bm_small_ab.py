@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import Codec, fill_random, set_knob  # noqa: E402
 
 
 def env_list(name, default, conv=str):
@@ -36,9 +36,9 @@ OPS = env_list("AB_OPS", ["enc_split", "enc_inplace", "dec_inplace"])
 
 def setenv(name, v):
     if v == "-":
-        os.environ.pop(name, None)
+        set_knob(name, None)
     else:
-        os.environ[name] = v
+        set_knob(name, v)
 
 
 def main():

@@ -15,7 +15,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import Codec, fill_random, set_knob  # noqa: E402
 
 ARMS = [("default", None), ("uncapped", "0")]
 # CAP_ARMS="64:12,256:16,..." = MEC_BLOCK:MEC_WPC pairs ("-" leaves a knob unset)
@@ -54,9 +54,9 @@ def main():
             for arm, (blk, wpc) in arms:
                 for var, val in (("MEC_BLOCK", blk), ("MEC_WPC", wpc)):
                     if val == "-":
-                        os.environ.pop(var, None)
+                        set_knob(var, None)
                     else:
-                        os.environ[var] = val
+                        set_knob(var, val)
                 step()
                 ev[0].record()
                 for _ in range(10):
@@ -64,8 +64,8 @@ def main():
                 ev[1].record()
                 ev[1].synchronize()
                 res[arm].append(ev[0].elapsed_time(ev[1]) / 10)
-        os.environ.pop("MEC_WPC", None)
-        os.environ.pop("MEC_BLOCK", None)
+        set_knob("MEC_WPC", None)
+        set_knob("MEC_BLOCK", None)
         pct = {a: nbytes / (statistics.median(v) * 1e-3) / 8e12 * 100 for a, v in res.items()}
         if GRID:
             best = max(pct, key=pct.get)

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import Codec, fill_random, set_knob  # noqa: E402
 
 K, M, CS, N = 10, 4, 1 << 20, 4096
 
@@ -54,7 +54,7 @@ def main():
         for name, step, nb in base:
             for cap in caps:
                 def capped(step=step, cap=cap):
-                    os.environ["MEC_WPC"] = cap
+                    set_knob("MEC_WPC", cap)
                     step()
                 arms.append(("%s wpc=%s" % (name, cap), capped, nb))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]

@@ -17,8 +17,9 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from cap_ab import workload  # noqa: E402
+from memec_amd import set_knob  # noqa: E402
 
-KNOBS = ("MEC_BLOCK", "MEC_WINDOWS", "MEC_WPC", "MEC_BM_VW", "MEC_ONES")
+KNOBS = ("MEC_BLOCK", "MEC_WINDOWS", "MEC_WPC", "MEC_BM_VW")
 
 
 def parse_arms(text):
@@ -44,8 +45,8 @@ def main():
         for _ in range(5):
             for arm, env in arms:
                 for k in KNOBS:
-                    os.environ.pop(k, None)
-                os.environ.update(env)
+                    set_knob(k, None)
+                [set_knob(_k, _v) for _k, _v in env.items()]
                 step()
                 ev[0].record()
                 for _ in range(10):
@@ -54,7 +55,7 @@ def main():
                 ev[1].synchronize()
                 res[arm].append(ev[0].elapsed_time(ev[1]) / 10)
         for k in KNOBS:
-            os.environ.pop(k, None)
+            set_knob(k, None)
         pct = {a: nbytes / (statistics.median(v) * 1e-3) / 8e12 * 100 for a, v in res.items()}
         best = max(pct, key=pct.get)
         print("%-13s " % name + " ".join("%s %5.1f" % (a, pct[a]) for a, _ in arms) +

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import Codec, fill_random, set_knob  # noqa: E402
 
 KNOBS = ("MEC_GBLOCK", "MEC_GWPC", "MEC_WPC", "MEC_BLOCK")
 # (family, k, m, chunk, stripes, slot header; -1 = one contiguous [stripe][k+m][chunk] buffer, op)
@@ -68,8 +68,8 @@ def main():
         for _ in range(5):
             for arm, env in arms:
                 for kn in KNOBS:
-                    os.environ.pop(kn, None)
-                os.environ.update(env)
+                    set_knob(kn, None)
+                [set_knob(_k, _v) for _k, _v in env.items()]
                 call()
                 ev[0].record()
                 for _ in range(8):
@@ -78,7 +78,7 @@ def main():
                 ev[1].synchronize()
                 res[arm].append(ev[0].elapsed_time(ev[1]) / 8)
         for kn in KNOBS:
-            os.environ.pop(kn, None)
+            set_knob(kn, None)
         nbytes = n * (k + m) * cs  # encode: k + m chunks; decode of 4 erasures at m = 4: k + 4
         print("%-6s %-6s k=%-2d m=%d cs=%-7d hdr=%-3d " % (op, fam, k, m, cs, hdr) +
               " ".join("%s %6.1f GB/s" % (a, nbytes / (statistics.median(v) * 1e-3) / 1e9) for a, v in res.items()),

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import Codec, fill_random, set_knob  # noqa: E402
 
 FAM, K, M = os.environ.get("SG_CODE", "rs,10,4").split(",")
 K, M = int(K), int(M)
@@ -25,9 +25,9 @@ TOTAL = 56 << 30
 
 def set_group(v):
     if v == "d":  # the library's own rule
-        os.environ.pop("MEC_SGROUP", None)
+        set_knob("MEC_SGROUP", None)
     else:
-        os.environ["MEC_SGROUP"] = v
+        set_knob("MEC_SGROUP", v)
 
 
 def main():
@@ -57,7 +57,7 @@ def main():
                           st[:, :4], (K + 4) * cs * n))
     # correctness: every group value gives the identity map's bytes
     for name, c, step, out, _ in cases:
-        os.environ["MEC_SGROUP"] = "0"
+        set_knob("MEC_SGROUP", "0")
         step()
         torch.cuda.synchronize()
         ref = out.clone()

@@ -11,7 +11,7 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
 from bench import CONFIGS  # noqa: E402
-from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import Codec, fill_random, set_knob  # noqa: E402
 
 
 def run(cfg, rounds=5, wins=(1, 2, 4), var="MEC_WINDOWS"):
@@ -39,7 +39,7 @@ def run(cfg, rounds=5, wins=(1, 2, 4), var="MEC_WINDOWS"):
     res = {w: [] for w in wins}
     for _ in range(rounds):
         for w in wins:
-            os.environ[var] = str(w)
+            set_knob(var, str(w))
             step()
             ev[0].record()
             for _ in range(10):

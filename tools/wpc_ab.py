@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-from memec_amd import Codec, fill_random  # noqa: E402
+from memec_amd import Codec, fill_random, set_knob  # noqa: E402
 
 CASES = [("rs", 4, 2), ("rs", 8, 2), ("rs", 12, 2), ("rs", 10, 4), ("cauchy", 4, 2), ("cauchy", 8, 2),
          ("cauchy", 12, 4)]
@@ -57,9 +57,9 @@ def main():
                 for _ in range(5):
                     for w in WPC:
                         if w < 0 or (VAR != "MEC_WPC" and w == 0):  # -1: the library's default
-                            os.environ.pop(VAR, None)
+                            set_knob(VAR, None)
                         else:
-                            os.environ[VAR] = str(w)
+                            set_knob(VAR, str(w))
                         step()
                         ev[0].record()
                         for _ in range(8):
@@ -67,7 +67,7 @@ def main():
                         ev[1].record()
                         ev[1].synchronize()
                         res[w].append(ev[0].elapsed_time(ev[1]) / 8)
-                os.environ.pop(VAR, None)
+                set_knob(VAR, None)
                 pct = {w: nbytes / (statistics.median(v) * 1e-3) / 8e12 * 100 for w, v in res.items()}
                 best = max(pct, key=pct.get)
                 print("%-6s %-6s k=%-2d m=%d cs=%-7d " % (op, fam, k, m, cs) +

@@ -10,7 +10,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-from memec_amd import fill_random, xor  # noqa: E402
+from memec_amd import fill_random, xor, set_knob  # noqa: E402
 
 
 def main():
@@ -30,11 +30,11 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     for _ in range(rounds):
         for bt, w in arms:
-            os.environ["MEC_BLOCK"] = bt
+            set_knob("MEC_BLOCK", bt)
             if w is None:
-                os.environ.pop("MEC_WPC", None)
+                set_knob("MEC_WPC", None)
             else:
-                os.environ["MEC_WPC"] = w
+                set_knob("MEC_WPC", w)
             xor(o, a, b)
             ev[0].record()
             for _ in range(5):
