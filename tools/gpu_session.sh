@@ -33,10 +33,12 @@ for step in "$@"; do
         tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py ;;
+        benchdec) run bench_rs_dec 400 python bench.py --config rs_dec ;;
         benchall)
             for c in rs_enc rs_dec rs_dec_mixed rs8_small crs_enc crs_dec rs42 rs42_dec rs_update rs8_update; do
                 run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 10
             done ;;
+        cpu256) run bench_cpu256 400 python bench.py --cpu-threads 256 --no-extra-configs --no-secondary --steps 10 ;;
         batch) run bench_batch 600 python tools/bench_batch.py ;;
         e2e) run bench_e2e 400 python bench.py --e2e --no-cpu-baseline --no-extra-configs --steps 5 ;;
         prof)
