@@ -531,6 +531,36 @@ def twin_rate(codec, step, alg_bytes, reps=5):
     return alg_bytes / (best * 1e-3) / 1e9
 
 
+def box_info(dev):
+    """Which box this ran on, for box-to-box comparisons (the
+    configs[4] decode runs in one of two modes): the device's UUID from
+    torch, and clocks / firmware / VBIOS from rocm-smi run as a child
+    process (None fields if it is absent or slow)."""
+    import subprocess
+    import torch
+    p = torch.cuda.get_device_properties(dev)
+    info = {"gpu_uuid": str(getattr(p, "uuid", "")), "name": p.name, "cus": p.multi_processor_count}
+    # not under a profiler: its preloaded library initialises the GPU in
+    # every process it starts, and rocm-smi's #!/usr/bin/env launcher then
+    # re-execs (refused on the GPU boxes)
+    if any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ) or "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        info["smi_error"] = "skipped under rocprofv3"
+        return info
+    try:
+        out = subprocess.run(["rocm-smi", "--showclocks", "--showfwinfo", "--showvbios", "--json"],
+                             capture_output=True, text=True, timeout=30)
+        cards = json.loads(out.stdout)
+        cards = {c: v for c, v in cards.items() if c.startswith("card")}
+        info["smi_cards"] = len(cards)
+        if cards:
+            v = cards[sorted(cards)[0]]
+            keep = ("mclk", "sclk", "fclk", "socclk", "vbios", "smc", "psp sos", "mec", "rlc", "sdma", "ta ras")
+            info["smi"] = {k: x for k, x in v.items() if any(t in k.lower() for t in keep)}
+    except Exception as exc:  # informational only
+        info["smi_error"] = repr(exc)[:200]
+    return info
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -1046,6 +1076,7 @@ def main():
             line["decode_verified" if op == "decode" else "update_verified"] = ok
         if dist_info:
             line["dist"] = dist_info
+        line["box"] = box_info(dev)
         if e2e:
             line["e2e_host_memory"] = e2e
         if extras:

@@ -59,6 +59,12 @@ for step in "$@"; do
                     SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
                     --output-format csv -d "$OUT/pmc_sq_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 3 --warmup 1
             done ;;
+        sqlds)
+            for c in ${PROF_CONFIGS:-rs_enc}; do
+                run "pmc_sqlds_$c" 400 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT \
+                    SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
+                    --output-format csv -d "$OUT/pmc_sqlds_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --no-extra-configs --no-ceiling --steps 3 --warmup 1
+            done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
