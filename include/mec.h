@@ -114,6 +114,11 @@ typedef struct {
     uint64_t staged_calls;       /* host calls copied through pinned, GPU-mapped staging */
     uint64_t queue_calls;        /* zero-copy calls served by the resident queue kernel */
     uint64_t queue_launches;     /* launches of the resident queue kernel (idle exits relaunch) */
+    uint32_t queue_slots;        /* slots actually running (mec_set_host_queue may grant fewer) */
+    uint32_t queue_parts;        /* workgroups per slot (one per 16 KiB of chunk, at most 8) */
+    uint32_t queue_broken;       /* 1: a call timed out and the queue stopped for good */
+    uint32_t pad0;
+    uint64_t queue_timeouts;     /* calls that hit MEC_QUEUE_TIMEOUT_MS */
 } mec_stats;
 
 typedef struct {
@@ -279,18 +284,31 @@ int mec_encode_update_batch(mec_ctx *ctx, const uint32_t *data_index, const uint
 int mec_set_coalescing(mec_ctx *ctx, uint32_t max_batch);
 
 /* Device-side submission queue for single-stripe host calls (queue.hip).
- * slots > 0 starts a resident kernel with one workgroup per slot, polling
+ * slots > 0 starts a resident kernel with `parts` workgroups per slot (one
+ * per 16 KiB of chunk, at most 8; MEC_QUEUE_PARTS overrides), polling
  * GPU-mapped host memory; mec_encode_host / mec_decode_host /
- * mec_encode_update_host calls of a byte-wise family (RS, ISA-L) with
- * chunks of at most MEC_QUEUE_MAX_CHUNK bytes (default 16 KiB) are then
- * posted to a free slot instead of launching a kernel: no HIP runtime call
- * on the caller's path (calls beyond `slots` concurrent callers take the
- * launch path).  Registered chunks (mec_host_register) are coded in place;
- * other host chunks are copied through a mapped pinned staging buffer.  The
- * kernel exits after MEC_QUEUE_IDLE_MS (default 50) without work and is
- * relaunched by the next call.  0 stops it.  Not to be called concurrently
- * with other calls on the context.  Replaces nothing in the reference: its
- * workers call the CPU plugin directly (worker.cc:128-137). */
+ * mec_encode_update_host calls of every family (RS and ISA-L byte-wise,
+ * Jerasure Cauchy-RS as bitmatrix jobs) with chunks of at most
+ * MEC_QUEUE_MAX_CHUNK bytes are then posted to a free slot instead of
+ * launching a kernel: no HIP runtime call on the caller's path (calls
+ * beyond `slots` concurrent callers take the launch path).  Registered
+ * chunks (mec_host_register) are coded in place; other host chunks are
+ * copied through a mapped pinned staging buffer.
+ * Slots: every workgroup must be resident at once, so `slots` is reduced to
+ * what the device can hold (mec_stats.queue_slots reports the number
+ * running; the call still returns MEC_OK).
+ * Idle: the kernel exits after MEC_QUEUE_IDLE_MS (default 50) without work
+ * and is relaunched by the next call.
+ * Timeout: a call not completed within MEC_QUEUE_TIMEOUT_MS (default 5000)
+ * withdraws its job, stops the queue FOR GOOD (mec_stats.queue_broken = 1,
+ * queue_timeouts counts them; every later call takes the launch path until
+ * mec_set_host_queue is called again) and waits — without a time limit —
+ * until the resident kernel has left, so no queue work can still write the
+ * caller's chunks when the call returns; a job that never ran is then coded
+ * on the launch path.
+ * 0 stops the queue.  Not to be called concurrently with other calls on the
+ * context.  Replaces nothing in the reference: its workers call the CPU
+ * plugin directly (worker.cc:128-137). */
 int mec_set_host_queue(mec_ctx *ctx, uint32_t slots);
 int mec_get_stats(const mec_ctx *ctx, mec_stats *out);
 

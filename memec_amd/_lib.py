@@ -41,7 +41,9 @@ class MecStats(ctypes.Structure):
     _fields_ = [("coalesced_batches", ctypes.c_uint64), ("coalesced_requests", ctypes.c_uint64),
                 ("cached_plans", ctypes.c_uint64), ("zero_copy_calls", ctypes.c_uint64),
                 ("staged_calls", ctypes.c_uint64), ("queue_calls", ctypes.c_uint64),
-                ("queue_launches", ctypes.c_uint64)]
+                ("queue_launches", ctypes.c_uint64), ("queue_slots", ctypes.c_uint32),
+                ("queue_parts", ctypes.c_uint32), ("queue_broken", ctypes.c_uint32), ("pad0", ctypes.c_uint32),
+                ("queue_timeouts", ctypes.c_uint64)]
 
 
 _lib = None

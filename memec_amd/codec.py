@@ -210,7 +210,9 @@ class Codec:
         return {"coalesced_batches": st.coalesced_batches, "coalesced_requests": st.coalesced_requests,
                 "cached_plans": st.cached_plans, "zero_copy_calls": st.zero_copy_calls,
                 "staged_calls": st.staged_calls, "queue_calls": st.queue_calls,
-                "queue_launches": st.queue_launches}
+                "queue_launches": st.queue_launches, "queue_slots": st.queue_slots,
+                "queue_parts": st.queue_parts, "queue_broken": bool(st.queue_broken),
+                "queue_timeouts": st.queue_timeouts}
 
 
 def fill_random(t, seed, word_offset=0, stream=None):

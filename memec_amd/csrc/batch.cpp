@@ -917,6 +917,10 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
     out->staged_calls = c->staged_calls.load();
     out->queue_calls = c->hq ? c->hq->calls.load() : 0;
     out->queue_launches = c->hq ? c->hq->launches.load() : 0;
+    out->queue_slots = c->hq ? c->hq->slots : 0;
+    out->queue_parts = c->hq ? c->hq->parts : 0;
+    out->queue_broken = c->hq && c->hq->broken.load() ? 1u : 0u;
+    out->queue_timeouts = c->hq ? c->hq->timeouts.load() : 0;
     {
         std::lock_guard<std::mutex> pk(c->plan_mu);
         out->cached_plans = c->plans.size();
@@ -931,6 +935,10 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
         out->staged_calls += t.staged_calls;
         out->queue_calls += t.queue_calls;
         out->queue_launches += t.queue_launches;
+        out->queue_slots += t.queue_slots;
+        out->queue_parts = std::max(out->queue_parts, t.queue_parts);
+        out->queue_broken |= t.queue_broken;
+        out->queue_timeouts += t.queue_timeouts;
     }
     return MEC_OK;
 }

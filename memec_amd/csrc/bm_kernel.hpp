@@ -220,7 +220,12 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
                 p.nstr = ns;
                 p.sgroup = stripe_group(p.chunk, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, true, p.srun);
-                const uint32_t lds = occupancy_lds(bt, std::min<uint32_t>(bt, g.units), 0, bm_target_waves(R, W, VW, p.win > 1));
+                const bool in_place = p.win > 1;
+                if (p.sgroup == kStripePerm) {  // the permutation replaces the windows
+                    p.win = 1;
+                    p.sgroup = stripe_group(p.chunk, g.tiles, ns, in_place, true, p.srun);
+                }
+                const uint32_t lds = occupancy_lds(bt, std::min<uint32_t>(bt, g.units), 0, bm_target_waves(R, W, VW, in_place));
                 if (bt == kWaveBlock)
                     hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock, VW>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
                 else

@@ -107,12 +107,13 @@ struct Coalescer {
 
 // queue.hip: device-side submission queue for single-stripe host calls.
 constexpr uint32_t kQMaxSrc = 32, kQMaxDst = 4, kQMaxSlots = 1024;
+constexpr uint32_t kQMaxParts = 8;  // workgroups per slot (one call's chunk spread over CUs)
 constexpr uint32_t kQBmRows = kQMaxDst * 8;  // bitmatrix output packet rows (outputs x w <= 8)
 struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
     uint64_t seq;            // host -> GPU: number of the posted job
     uint64_t pad0[15];
-    uint64_t done;           // GPU -> host: number of the last finished job
-    uint64_t pad1[15];
+    uint64_t done[kQMaxParts];  // GPU -> host: number of the last job each part finished
+    uint64_t pad1[16 - kQMaxParts];
     // sources, outputs, chunk bytes, accumulate, w (0: byte-wise GF(2^8);
     // 1..8: Jerasure bitmatrix over w packets), packet bytes, -, -
     uint32_t hdr[8];
@@ -127,7 +128,13 @@ struct HostQueue {
     QSlot *host = nullptr, *dev = nullptr;
     uint32_t *ctl_host = nullptr, *ctl_dev = nullptr;  // [kQCtlStop] host -> GPU, [kQCtlExit] leader -> grid
     uint64_t *act = nullptr;          // device memory: per-slot time of the last job (s_memrealtime)
-    uint32_t slots = 0, max_chunk = 0, threads = 0;
+    // device memory, per slot: [0, slots) the job part 0 took (`go`, read by
+    // the slot's other parts), [slots, 2 slots) the launch epoch in which
+    // part 0 left the grid (`left`: the other parts leave after it)
+    uint64_t *link = nullptr;
+    uint64_t epoch = 0;               // launches so far (the `left` epoch)
+    uint32_t slots = 0, parts = 1, max_chunk = 0, threads = 0;
+    std::atomic<uint64_t> timeouts{0};  // calls that timed out (each stops the queue for good)
     uint32_t solo_max = 0;            // larger chunks use the queue only beside other queue calls
     std::atomic<uint32_t> inflight{0};
     std::atomic<bool> broken{false};  // a call timed out: the queue is stopped for good

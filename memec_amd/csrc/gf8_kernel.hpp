@@ -277,8 +277,13 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                 p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
                 p.nstr = ns;
                 p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
+                const bool in_place = p.win > 1;
+                if (p.sgroup == kStripePerm) {  // the permutation replaces the windows
+                    p.win = 1;
+                    p.sgroup = stripe_group(L.len, g.tiles, ns, in_place, false, p.srun);
+                }
                 const dim3 grid(ns * g.tiles), block(bt);
-                const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, p.win > 1, !vand, L.accumulate));
+                const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, in_place, !vand, L.accumulate));
                 if (L.probe) {
                     if (bt == kWaveBlock)
                         hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Xor, kWaveBlock>), grid, block, lds, stream, p);

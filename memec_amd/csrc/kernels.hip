@@ -235,6 +235,21 @@ uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool i
     uint32_t g = (!bitmatrix && chunk >= (uint64_t(2) << 20)) ? 16u : 0u;
     if (kg != kKnobUnset) {
         if (kg == kKnobXcd) return tiles % 8 == 0 ? kXcdRegions : 0u;
+        if (kg == kKnobPerm) {  // a multiplier coprime to n_stripes near n / golden ratio
+            if (n_stripes < 2) return 0;
+            uint64_t mlt = kr != kKnobUnset && kr > 0 ? uint64_t(kr) : uint64_t(double(n_stripes) * 0.6180339887) | 1u;
+            auto gcd = [](uint64_t a, uint64_t b) {
+                while (b) {
+                    const uint64_t t = a % b;
+                    a = b;
+                    b = t;
+                }
+                return a;
+            };
+            while (gcd(mlt % n_stripes, n_stripes) != 1) mlt += 1;
+            run = uint32_t(mlt % n_stripes);
+            return kStripePerm;
+        }
         g = uint32_t(std::max<int64_t>(kg, 0));
         if (kr != kKnobUnset) run = uint32_t(std::max<int64_t>(kr, 0));
     }

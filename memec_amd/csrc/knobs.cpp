@@ -29,6 +29,9 @@ struct Knobs {
             } else if (value[0] == 'x') {
                 put(kKnobSgroup, kKnobXcd);
                 put(kKnobSrun, kKnobUnset);
+            } else if (value[0] == 'p') {
+                put(kKnobSgroup, kKnobPerm);
+                put(kKnobSrun, value[1] ? int64_t(std::atoll(value + 1)) : kKnobUnset);
             } else {
                 put(kKnobSgroup, num);
                 const char *c = std::strchr(value, ':');

@@ -42,6 +42,7 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -239,17 +240,29 @@ __device__ __forceinline__ void mark_active(uint64_t *act) {
 
 constexpr uint32_t kQDescWords = 8 + 2 * (kQMaxSrc + kQMaxDst) + kQMaxDst * kQMaxSrc / 4 + kQMaxSrc * kQBmRows / 4;
 
-__global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t *ctl, uint64_t *act,
-                                                         uint64_t idle_ticks, uint32_t nthr, uint32_t nslots) {
+// Workgroup b serves slot b / parts as part b % parts: part 0 polls the
+// slot in host memory and, when it takes a job, publishes its number in
+// device memory (`go`), where the slot's other parts poll; every part codes
+// its share of the units (16-byte units part, part + parts, ... of each
+// nthr-thread pass) and stores its own done word.  Part 0 alone watches the
+// control words; when it leaves it records the launch epoch in `left`, and
+// the other parts leave only after that, having run every job part 0 took
+// — so a job is run by all of a slot's parts or by none (a withdrawn job
+// is never taken, queue_try).
+__global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t *ctl, uint64_t *act, uint64_t *link,
+                                                         uint64_t epoch, uint64_t idle_ticks, uint32_t nthr,
+                                                         uint32_t nslots, uint32_t parts) {
     __shared__ uint32_t desc[kQDescWords];  // the slot's descriptor: hdr, src, dst, coef_w, mask_w
     __shared__ uint32_t tab[kQMaxDst * kQMaxSrc * 8];
     __shared__ uint32_t cmd;
-    QSlot *s = slots + blockIdx.x;
+    const uint32_t si = blockIdx.x / parts, part = blockIdx.x - si * parts;
+    QSlot *s = slots + si;
+    uint64_t *go = link + si, *left = link + nslots + si;
     const uint32_t t = threadIdx.x;
     const bool leader = blockIdx.x == 0;
     uint64_t last = 0, t0 = 0;
     if (t == 0) {
-        last = sys_load(&s->done);
+        last = sys_load(&s->done[part]);
         t0 = __builtin_amdgcn_s_memrealtime();
     }
     const uint32_t *hdr = desc;
@@ -257,13 +270,28 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
     const uint32_t *cw = desc + 8 + 2 * (kQMaxSrc + kQMaxDst);
     const uint8_t *mk = reinterpret_cast<const uint8_t *>(cw + kQMaxDst * kQMaxSrc / 4);
     for (;;) {
-        if (t == 0) {
+        if (t == 0 && part != 0) {  // the other parts: part 0's jobs, from device memory
+            uint32_t c = 0;
+            for (;;) {
+                const uint64_t lf = __hip_atomic_load(left, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t q = __hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                if (q > last) {
+                    last = q;
+                    c = 1;
+                    break;
+                }
+                if (lf == epoch) break;  // part 0 has left and every job it took has run here
+                __builtin_amdgcn_s_sleep(2);
+            }
+            cmd = c;
+        } else if (t == 0) {
             uint32_t c = 0;
             for (uint32_t n = 1;; ++n) {  // one PCIe read per poll; control words every 64th
                 const uint64_t q = __hip_atomic_load(&s->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (q > last) {  // a withdrawn job moves seq back (queue_try)
                     last = q;
                     c = 1;
+                    if (parts > 1) __hip_atomic_store(go, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
                 if (n % 64 == 0) {
@@ -283,7 +311,8 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                 __builtin_amdgcn_s_sleep(4);
             }
             cmd = c;
-            if (c) mark_active(act + blockIdx.x);
+            if (c) mark_active(act + si);
+            else if (parts > 1) __hip_atomic_store(left, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
         __syncthreads();
         if (cmd == 0) return;  // uniform: stop or grid idle
@@ -305,29 +334,31 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                 T[4] = pack4(c, 0, 64, 128, 192);
             }
             __syncthreads();
-            const uint32_t full = bytes / 16;
-            for (uint32_t u = t; u < full; u += nthr)
+            // this part's units: passes of nthr units, part-th of every parts
+            const uint32_t full = bytes / 16, me = part * nthr + t, step = parts * nthr;
+            for (uint32_t u = me; u < full; u += step)
                 code_unit<true>(addr, tab, ns, nd, acc_in, uint64_t(u) * 16, 16);
-            if (bytes % 16 && t == full % nthr)  // the partial last unit
+            if (bytes % 16 && me == full % step)  // the partial last unit
                 code_unit<false>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
         } else {
+            const uint32_t me = part * nthr + t, step = parts * nthr;
             switch (w) {  // uniform
-                case 1: bm_job<1>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
-                case 2: bm_job<2>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
-                case 3: bm_job<3>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
-                case 4: bm_job<4>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
-                case 5: bm_job<5>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
-                case 6: bm_job<6>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
-                case 7: bm_job<7>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
-                case 8: bm_job<8>(addr, mk, ns, nd, acc_in, P, t, nthr); break;
+                case 1: bm_job<1>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 2: bm_job<2>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 3: bm_job<3>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 4: bm_job<4>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 5: bm_job<5>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 6: bm_job<6>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 7: bm_job<7>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 8: bm_job<8>(addr, mk, ns, nd, acc_in, P, me, step); break;
                 default: break;
             }
         }
         __threadfence_system();  // this lane's outputs reach host memory ...
-        __syncthreads();         // ... before the slot is marked done
+        __syncthreads();         // ... before the part is marked done
         if (t == 0) {
-            __hip_atomic_store(&s->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            mark_active(act + blockIdx.x);
+            __hip_atomic_store(&s->done[part], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (part == 0) mark_active(act + si);
         }
     }
 }
@@ -341,8 +372,9 @@ uint64_t env_u64(const char *name, uint64_t dflt) {
 int queue_launch(mec_ctx *c, HostQueue *q) {
     DeviceGuard dg(c->device);
     __atomic_store_n(q->ctl_host + kQCtlExit, 0u, __ATOMIC_RELEASE);
-    hipLaunchKernelGGL(queue_kernel, dim3(q->slots), dim3(q->threads), 0, q->stream, q->dev, q->ctl_dev, q->act,
-                       q->idle_ticks, q->threads, q->slots);
+    ++q->epoch;
+    hipLaunchKernelGGL(queue_kernel, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev, q->ctl_dev,
+                       q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts);
     HIP_TRY(hipGetLastError());
     q->launches++;
     return MEC_OK;
@@ -365,7 +397,7 @@ bool queue_drained(HostQueue *q, int ms) {
     const auto t0 = std::chrono::steady_clock::now();
     while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(ms)) {
         const hipError_t e = hipStreamQuery(q->stream);
-        if (e != hipErrorNotReady) return e == hipSuccess;
+        if (e != hipErrorNotReady) return true;  // finished (or failed: either way no longer running)
         std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
     return false;
@@ -384,6 +416,7 @@ void queue_stop(mec_ctx *c) {
         (void)hipStreamDestroy(q->stream);
         (void)hipHostFree(q->host);
         (void)hipFree(q->act);
+        (void)hipFree(q->link);
     }
     delete[] q->busy;
     delete q;
@@ -399,17 +432,24 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     q->solo_max = uint32_t(env_u64("MEC_QUEUE_SOLO_MAX", q->max_chunk));
     q->idle_ticks = env_u64("MEC_QUEUE_IDLE_MS", 50) * 100000ull;  // s_memrealtime: 100 MHz
     q->timeout_ms = env_u64("MEC_QUEUE_TIMEOUT_MS", 5000);
+    // workgroups per slot: one per 16 KiB of chunk (a kQThreads pass of
+    // 16-byte units), at most kQMaxParts, so a 64 KiB call is spread over 4
+    // CUs; MEC_QUEUE_PARTS overrides (A/Bs)
+    const uint32_t units = (c->cs + 15) / 16;
+    const uint32_t auto_parts = std::min<uint32_t>(kQMaxParts, std::max<uint32_t>(1, (units + kQThreads - 1) / kQThreads));
+    q->parts = std::min<uint32_t>(kQMaxParts, std::max<uint64_t>(1, env_u64("MEC_QUEUE_PARTS", auto_parts)));
     // one 16-byte unit per thread up to kQThreads (a 4 KiB chunk: 256 threads;
     // idle threads only cost barrier time), at least 128 (descriptor loads)
-    q->threads = std::min<uint32_t>(kQThreads, std::max<uint32_t>(128, (c->cs / 16 + 63) / 64 * 64));
-    // every slot's workgroup must be resident at once: a slot whose
+    const uint32_t per_part = (units + q->parts - 1) / q->parts;
+    q->threads = std::min<uint32_t>(kQThreads, std::max<uint32_t>(128, (per_part + 63) / 64 * 64));
+    // every workgroup of every slot must be resident at once: a slot whose
     // workgroup waits for another to exit would never be served
     {
         int per_cu = 0, cus = 0;
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_kernel, int(q->threads), 0));
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-        const uint32_t cap = uint32_t(std::max(1, per_cu * cus));
-        slots = std::min(slots, cap);
+        const uint32_t cap = uint32_t(std::max(1, per_cu * cus)) / q->parts;
+        slots = std::max<uint32_t>(1, std::min(slots, cap));
     }
     q->slots = slots;
     const size_t bytes = sizeof(QSlot) * slots + 256;
@@ -419,10 +459,11 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     void *d = nullptr;
     hipError_t e = hipHostGetDevicePointer(&d, h, 0);
     if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&q->act), sizeof(uint64_t) * slots);
-    if (e == hipSuccess) e = hipMemset(q->act, 0, sizeof(uint64_t) * slots);
+    if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&q->link), sizeof(uint64_t) * 2 * slots);
     if (e != hipSuccess) {
         (void)hipHostFree(h);
         if (q->act) (void)hipFree(q->act);
+        if (q->link) (void)hipFree(q->link);
         return hip_fail(e, "queue memory");
     }
     q->host = static_cast<QSlot *>(h);
@@ -432,11 +473,20 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     q->busy = new std::atomic<bool>[slots];
     for (uint32_t i = 0; i < slots; ++i) q->busy[i].store(false);
     e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking);
+    // the zeroed per-slot words must be in place before the kernel reads
+    // them: a hipMemset need not have finished when work on a non-blocking
+    // stream starts, and a reused allocation still holds an earlier queue's
+    // `go` numbers (which made a part skip a job)
+    if (e == hipSuccess) e = hipMemsetAsync(q->act, 0, sizeof(uint64_t) * slots, q->stream);
+    if (e == hipSuccess) e = hipMemsetAsync(q->link, 0, sizeof(uint64_t) * 2 * slots, q->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(q->stream);
     if (e != hipSuccess) {
+        if (q->stream) (void)hipStreamDestroy(q->stream);
         (void)hipHostFree(h);
         (void)hipFree(q->act);
+        (void)hipFree(q->link);
         delete[] q->busy;
-        return hip_fail(e, "hipStreamCreate");
+        return hip_fail(e, "queue stream");
     }
     {
         std::lock_guard<std::mutex> g(q->mu);
@@ -445,6 +495,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
             (void)hipStreamDestroy(q->stream);
             (void)hipHostFree(h);
             (void)hipFree(q->act);
+            (void)hipFree(q->link);
             delete[] q->busy;
             return rc;
         }
@@ -499,28 +550,34 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     bool taken = true;
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t spins = 0;
-    while (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) != seq) {
+    auto finished = [&] {  // every part of the slot has stored this job's number
+        for (uint32_t p = 0; p < q->parts; ++p)
+            if (__atomic_load_n(&s->done[p], __ATOMIC_ACQUIRE) != seq) return false;
+        return true;
+    };
+    while (!finished()) {
         if (++spins % 2048 == 0 || q->timeout_ms == 0) {
             const auto dt = std::chrono::steady_clock::now() - t0;
             if (dt > std::chrono::milliseconds(q->timeout_ms) || q->broken.load()) {
-                // Withdraw the job (seq moves back: a workgroup that has not
-                // taken it never will, one that has runs the unchanged
-                // descriptor to the end), stop the queue for good, and wait
-                // for the grid to leave.  Then done == seq means the job ran;
-                // otherwise nothing can touch the caller's chunks any more and
-                // the launch path codes them instead.
+                // Withdraw the job (seq moves back: a part 0 that has not
+                // taken it never will; once taken, every part runs the
+                // unchanged descriptor to the end), stop the queue for good,
+                // and wait for the whole grid to leave — however long that
+                // takes: until then a part may still write the caller's
+                // chunks.  Then done[0] == seq means the job ran (the other
+                // parts leave only after part 0, with its jobs done);
+                // otherwise nothing touched the chunks and the launch path
+                // codes them instead.
                 rc = MEC_OK;
+                if (dt > std::chrono::milliseconds(q->timeout_ms)) q->timeouts++;
                 __atomic_store_n(&s->seq, seq - 1, __ATOMIC_SEQ_CST);
                 q->broken.store(true);
                 __atomic_store_n(q->ctl_host + kQCtlStop, 1u, __ATOMIC_RELEASE);
-                const bool drained = queue_drained(q, 1000);
-                if (__atomic_load_n(&s->done, __ATOMIC_ACQUIRE) == seq) break;  // it ran after all
-                if (drained) {
-                    taken = false;
-                } else {
-                    rc = fail(MEC_EHIP, "host queue: no completion within %llu ms and the grid did not stop",
-                              (unsigned long long)q->timeout_ms);
-                }
+                for (int waited = 0; !queue_drained(q, 5000); waited += 5)
+                    fprintf(stderr, "libmec: host queue stopped after a %llu ms call timeout; waiting for the "
+                                    "resident kernel to leave (%d s)\n",
+                            (unsigned long long)q->timeout_ms, waited + 5);
+                if (__atomic_load_n(&s->done[0], __ATOMIC_ACQUIRE) != seq) taken = false;  // never ran
                 break;
             }
             if (dt > std::chrono::microseconds(200)) std::this_thread::yield();

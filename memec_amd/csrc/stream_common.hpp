@@ -98,11 +98,21 @@ __device__ __forceinline__ uint32_t block_order(uint32_t win) {
 // tiles % run == 0 and run % 8 == 0 whenever group != 0 (host side,
 // stripe_group; `run` consecutive tiles per stripe visit, default 8).
 constexpr uint32_t kXcdRegions = 0xffffffffu;  // stripe_group value of MEC_SGROUP=x
+// stripe_group value of MEC_SGROUP=p[<mult>] (experiment): block q-th
+// stripe visit goes to stripe (q * run) mod ns, run coprime to ns, so the
+// blocks resident at once work on stripes scattered over the whole buffer
+constexpr uint32_t kStripePerm = 0xfffffffeu;
 __device__ __forceinline__ void stripe_tile(uint32_t bid, uint32_t tiles, uint32_t ns, uint32_t group, uint32_t run,
                                             uint32_t &stripe, uint32_t &tile) {
     if (group == 0) {
         stripe = bid / tiles;
         tile = bid - stripe * tiles;
+        return;
+    }
+    if (group == kStripePerm) {
+        const uint32_t q = bid / tiles;
+        tile = bid - q * tiles;
+        stripe = uint32_t((uint64_t(q) * run) % ns);
         return;
     }
     if (group == kXcdRegions) {  // experiment: XCD x (block id mod 8) takes the x-th eighth of each stripe

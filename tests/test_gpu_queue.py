@@ -87,11 +87,12 @@ def test_queue_cauchy_packet_tails(k, m, cs):
     _encode_decode_update("cauchy", k, m, cs)
 
 
-def _encode_decode_update(fam, k, m, cs):
+def _encode_decode_update(fam, k, m, cs, parts=1):
     slab = Slab(k + m + 1, cs, 31 + k)
     c = Codec(fam, k, m, cs)
     try:
         c.set_host_queue(8)
+        assert c.stats()["queue_parts"] == parts and c.stats()["queue_slots"] == 8
         data = [slab.view(j).copy() for j in range(k)]
         want = O.encode(fam, k, m, [d.copy() for d in data], cs)
         q0 = c.stats()["queue_calls"]
@@ -126,6 +127,79 @@ def _encode_decode_update(fam, k, m, cs):
             assert np.array_equal(slab.view(k + i), want2[i]), (fam, i)
         st = c.stats()
         assert st["queue_calls"] == q0 + m + 3 and st["queue_launches"] >= 1
+    finally:
+        c.close()
+        slab.close()
+
+
+@pytest.fixture
+def qenv():
+    """Queue settings read at mec_set_host_queue (never on a call path)."""
+    keys = []
+
+    def set_(**kv):
+        for k_, v in kv.items():
+            keys.append(k_)
+            os.environ[k_] = str(v)
+    yield set_
+    for k_ in keys:
+        os.environ.pop(k_, None)
+
+
+@pytest.mark.parametrize("fam", FAMILIES)
+@pytest.mark.parametrize("k,m,cs", [(10, 4, 65536), (12, 4, 32768), (4, 2, 65536 + 40), (6, 3, 20480 + 24)])
+def test_queue_multi_part_slots(fam, k, m, cs, qenv):
+    """Chunks above 16 KiB on the queue: one call's units are spread over
+    the slot's parts (workgroups on different CUs), each with its own done
+    word; partial units and bitmatrix packet tails land on the right part."""
+    qenv(MEC_QUEUE_MAX_CHUNK=128 << 10)
+    _encode_decode_update(fam, k, m, cs, parts=(cs // 16 + 1023) // 1024)
+
+
+@pytest.mark.parametrize("parts", [2, 3, 8])
+def test_queue_forced_parts(parts, qenv):
+    """MEC_QUEUE_PARTS splits even small chunks (uneven shares: 3 parts of
+    a 16 KiB chunk, 8 parts of a 4 KiB one leave some parts idle)."""
+    qenv(MEC_QUEUE_PARTS=parts)
+    for fam, k, m, cs in (("rs", 10, 4, 16384), ("cauchy", 8, 2, 4096)):
+        _encode_decode_update(fam, k, m, cs, parts=parts)
+
+
+def test_queue_multi_part_idle_exit_concurrent(qenv):
+    """Parts follow part 0 out of the grid (the `left` epoch) and back in
+    after a relaunch: 8 threads x 64 KiB calls, quiet gaps longer than the
+    idle timeout between bursts, every result checked."""
+    qenv(MEC_QUEUE_MAX_CHUNK=65536, MEC_QUEUE_IDLE_MS=3)
+    k, m, cs, T = 10, 4, 65536, 8
+    slab = Slab(T * (k + m), cs, 17)
+    c = Codec("rs", k, m, cs)
+    errs = []
+    try:
+        c.set_host_queue(8)
+        assert c.stats()["queue_parts"] == 4
+        wants = [O.encode("rs", k, m, [slab.view(t * (k + m) + j).copy() for j in range(k)], cs) for t in range(T)]
+
+        def worker(t):
+            try:
+                base = t * (k + m)
+                for n in range(12):
+                    i = n % m
+                    slab.view(base + k + i)[:] = 0
+                    encode_index(c, slab, k, [base + j for j in range(k)], base + k + i, i + 1)
+                    if not np.array_equal(slab.view(base + k + i), wants[t][i]):
+                        errs.append((t, n))
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+        for burst in range(3):
+            th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            time.sleep(0.05)  # the grid idles out
+        assert not errs, errs[:5]
+        st = c.stats()
+        assert st["queue_calls"] > 0 and st["queue_launches"] >= 2 and not st["queue_broken"]
     finally:
         c.close()
         slab.close()
@@ -257,6 +331,7 @@ def test_queue_timeout_withdraws_and_falls_back(fam):
                 encode_index(c, slab, k, list(range(k)), k + i, i + 1)
                 assert np.array_equal(slab.view(k + i), want[i]), (rnd, i)
         st = c.stats()
+        assert st["queue_broken"] and st["queue_timeouts"] >= 1
         assert st["queue_calls"] <= 1  # at most the first call, if it beat the withdrawal
         assert st["zero_copy_calls"] == 3 * m
         # staged calls on the broken queue take launches too
