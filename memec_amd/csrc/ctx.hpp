@@ -107,13 +107,12 @@ struct Coalescer {
 
 // queue.hip: device-side submission queue for single-stripe host calls.
 constexpr uint32_t kQMaxSrc = 32, kQMaxDst = 4, kQMaxSlots = 1024;
-constexpr uint32_t kQMaxParts = 8;  // workgroups per slot (one call's chunk spread over CUs)
+constexpr uint32_t kQMaxParts = 64;  // workgroups per slot (one call's chunk spread over CUs)
 constexpr uint32_t kQBmRows = kQMaxDst * 8;  // bitmatrix output packet rows (outputs x w <= 8)
 struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
     uint64_t seq;            // host -> GPU: number of the posted job
     uint64_t pad0[15];
     uint64_t done[kQMaxParts];  // GPU -> host: number of the last job each part finished
-    uint64_t pad1[16 - kQMaxParts];
     // sources, outputs, chunk bytes, accumulate, w (0: byte-wise GF(2^8);
     // 1..8: Jerasure bitmatrix over w packets), packet bytes, -, -
     uint32_t hdr[8];

@@ -323,8 +323,8 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
         __syncthreads();
         const uint32_t ns = hdr[0], nd = hdr[1], bytes = hdr[2], acc_in = hdr[3], w = hdr[4], P = hdr[5];
         if (w == 0) {  // byte-wise GF(2^8): v_perm tables from the coefficient bytes
-            if (t < nd * ns) {
-                const uint32_t r = t / ns, j = t - r * ns, b = r * kQMaxSrc + j;
+            for (uint32_t e = t; e < nd * ns; e += nthr) {  // nthr may be 64 (one-wave parts)
+                const uint32_t r = e / ns, j = e - r * ns, b = r * kQMaxSrc + j;
                 const uint32_t c = (cw[b / 4] >> (8 * (b % 4))) & 0xffu;
                 uint32_t *T = tab + b * 8;
                 T[0] = pack4(c, 0, 1, 2, 3);
@@ -432,16 +432,17 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     q->solo_max = uint32_t(env_u64("MEC_QUEUE_SOLO_MAX", q->max_chunk));
     q->idle_ticks = env_u64("MEC_QUEUE_IDLE_MS", 50) * 100000ull;  // s_memrealtime: 100 MHz
     q->timeout_ms = env_u64("MEC_QUEUE_TIMEOUT_MS", 5000);
-    // workgroups per slot: one per 16 KiB of chunk (a kQThreads pass of
-    // 16-byte units), at most kQMaxParts, so a 64 KiB call is spread over 4
-    // CUs; MEC_QUEUE_PARTS overrides (A/Bs)
+    // workgroups per slot: one per MEC_QUEUE_PART_THREADS units (default
+    // kQThreads: a 16 KiB pass of 16-byte units), at most kQMaxParts;
+    // MEC_QUEUE_PARTS sets the count directly (A/Bs)
     const uint32_t units = (c->cs + 15) / 16;
-    const uint32_t auto_parts = std::min<uint32_t>(kQMaxParts, std::max<uint32_t>(1, (units + kQThreads - 1) / kQThreads));
+    const uint32_t pthr = uint32_t(std::min<uint64_t>(kQThreads, std::max<uint64_t>(64, env_u64("MEC_QUEUE_PART_THREADS", kQThreads))));
+    const uint32_t auto_parts = std::min<uint32_t>(kQMaxParts, std::max<uint32_t>(1, (units + pthr - 1) / pthr));
     q->parts = std::min<uint32_t>(kQMaxParts, std::max<uint64_t>(1, env_u64("MEC_QUEUE_PARTS", auto_parts)));
     // one 16-byte unit per thread up to kQThreads (a 4 KiB chunk: 256 threads;
     // idle threads only cost barrier time), at least 128 (descriptor loads)
     const uint32_t per_part = (units + q->parts - 1) / q->parts;
-    q->threads = std::min<uint32_t>(kQThreads, std::max<uint32_t>(128, (per_part + 63) / 64 * 64));
+    q->threads = std::min<uint32_t>(kQThreads, std::max<uint32_t>(q->parts > 1 ? 64 : 128, (per_part + 63) / 64 * 64));
     // every workgroup of every slot must be resident at once: a slot whose
     // workgroup waits for another to exit would never be served
     {

@@ -156,6 +156,15 @@ def test_queue_multi_part_slots(fam, k, m, cs, qenv):
     _encode_decode_update(fam, k, m, cs, parts=(cs // 16 + 1023) // 1024)
 
 
+@pytest.mark.parametrize("pthr", [64, 256])
+def test_queue_one_wave_parts(pthr, qenv):
+    """Many small parts per slot (MEC_QUEUE_PART_THREADS): 64-thread parts
+    build their coefficient tables in several passes (4 x 32 > 64)."""
+    qenv(MEC_QUEUE_MAX_CHUNK=65536, MEC_QUEUE_PART_THREADS=pthr)
+    for fam, k, m, cs in (("rs", 20, 4, 32768), ("isal_cauchy", 12, 4, 16384), ("cauchy", 10, 4, 65536)):
+        _encode_decode_update(fam, k, m, cs, parts=min(64, (cs // 16 + pthr - 1) // pthr))
+
+
 @pytest.mark.parametrize("parts", [2, 3, 8])
 def test_queue_forced_parts(parts, qenv):
     """MEC_QUEUE_PARTS splits even small chunks (uneven shares: 3 parts of

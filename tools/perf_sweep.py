@@ -60,10 +60,14 @@ def one(fam, k, m, cs, target=2 << 30):
 
 
 def main():
+    """SWEEP_FAMS=cauchy SWEEP_KS=6,8,12 SWEEP_SIZES=2048,16384 narrow the grid."""
     torch.cuda.set_device(0)
-    for fam in ("rs", "cauchy"):
-        for k in (4, 6, 8, 12):
-            for cs in (2048, 4096, 8192, 16384, 32768, 65536, 131072):
+    fams = os.environ.get("SWEEP_FAMS", "rs,cauchy").split(",")
+    ks = [int(x) for x in os.environ.get("SWEEP_KS", "4,6,8,12").split(",")]
+    sizes = [int(x) for x in os.environ.get("SWEEP_SIZES", "2048,4096,8192,16384,32768,65536,131072").split(",")]
+    for fam in fams:
+        for k in ks:
+            for cs in sizes:
                 print(json.dumps(one(fam, k, 2, cs)), flush=True)
                 torch.cuda.empty_cache()
 
