@@ -272,10 +272,13 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
     for (;;) {
         if (t == 0 && part != 0) {  // the other parts: part 0's jobs, from device memory
             uint32_t c = 0;
+            // relaxed polls, one acquire fence per job taken: an acquire load
+            // per poll invalidated the L2 (buffer_inv) at every poll
             for (;;) {
-                const uint64_t lf = __hip_atomic_load(left, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-                const uint64_t q = __hip_atomic_load(go, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t lf = __hip_atomic_load(left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t q = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (q > last) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     last = q;
                     c = 1;
                     break;
@@ -287,8 +290,9 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
         } else if (t == 0) {
             uint32_t c = 0;
             for (uint32_t n = 1;; ++n) {  // one PCIe read per poll; control words every 64th
-                const uint64_t q = __hip_atomic_load(&s->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint64_t q = __hip_atomic_load(&s->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (q > last) {  // a withdrawn job moves seq back (queue_try)
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once per job
                     last = q;
                     c = 1;
                     if (parts > 1) __hip_atomic_store(go, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -354,8 +358,15 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                 default: break;
             }
         }
-        __threadfence_system();  // this lane's outputs reach host memory ...
-        __syncthreads();         // ... before the part is marked done
+        // Completion: every wave waits until its own output stores are
+        // acknowledged, the barrier orders that before thread 0, and thread
+        // 0's system-scope release store of `done` writes the L2 back once
+        // for the whole workgroup.  (A __threadfence_system per lane cost
+        // every wave an L2 writeback + invalidate per job, which made a
+        // 64 KiB call 2.4x slower on the queue than as a launch even with the
+        // launch's own geometry; profiles/r03/host/queue_pthr_ab.log.)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
         if (t == 0) {
             __hip_atomic_store(&s->done[part], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             if (part == 0) mark_active(act + si);

@@ -15,10 +15,10 @@ for cfg in "${CFGS[@]}"; do
     for arm in ${ARMS:-launch q1 qparts}; do
       case $arm in
         launch) env="MEMEC_GPU_QUEUE=0" ;;
-        q1) env="MEMEC_GPU_QUEUE=32 MEC_QUEUE_MAX_CHUNK=131072 MEC_QUEUE_PARTS=1" ;;
-        qparts) env="MEMEC_GPU_QUEUE=32 MEC_QUEUE_MAX_CHUNK=131072" ;;
-        qp256) env="MEMEC_GPU_QUEUE=32 MEC_QUEUE_MAX_CHUNK=131072 MEC_QUEUE_PART_THREADS=256" ;;
-        qp64) env="MEMEC_GPU_QUEUE=32 MEC_QUEUE_MAX_CHUNK=131072 MEC_QUEUE_PART_THREADS=64" ;;
+        q1) env="MEMEC_GPU_QUEUE=32 MEC_QUEUE_MAX_CHUNK=${QMAX:-131072} MEC_QUEUE_PARTS=1" ;;
+        qparts) env="MEMEC_GPU_QUEUE=32 MEC_QUEUE_MAX_CHUNK=${QMAX:-131072}" ;;
+        qp256) env="MEMEC_GPU_QUEUE=32 MEC_QUEUE_MAX_CHUNK=${QMAX:-131072} MEC_QUEUE_PART_THREADS=256" ;;
+        qp64) env="MEMEC_GPU_QUEUE=32 MEC_QUEUE_MAX_CHUNK=${QMAX:-131072} MEC_QUEUE_PART_THREADS=64" ;;
       esac
       env $env MEMEC_GPU_REGISTER=1 timeout -k 10 60 tools/coding_bench $1 $2 $3 $4 $w 2 $5 | sed "s/^{/{\"arm\": \"$arm\", /"
       rc=$?

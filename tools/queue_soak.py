@@ -31,6 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 os.environ.setdefault("MEC_QUEUE_IDLE_MS", "3")
+os.environ.setdefault("MEC_QUEUE_MAX_CHUNK", str(1 << 20))  # multi-part slots too
 import torch  # noqa: E402
 
 import _oracle as O  # noqa: E402
@@ -38,7 +39,10 @@ from test_gpu_queue import Slab, encode_index  # noqa: E402
 
 from memec_amd import Codec  # noqa: E402
 
-SHAPES = [("rs", 8, 2, 4096), ("cauchy", 12, 4, 4096), ("rs", 10, 4, 16384), ("cauchy", 6, 3, 8192)]
+SHAPES = [("rs", 8, 2, 4096), ("cauchy", 12, 4, 4096), ("rs", 10, 4, 16384), ("cauchy", 6, 3, 8192),
+          ("rs", 10, 4, 65536), ("cauchy", 12, 4, 65536)]  # the last two: 4-part slots
+if os.environ.get("SOAK_SHAPES"):  # fam:k:m:chunk,...
+    SHAPES = [(f, int(k), int(m), int(c)) for f, k, m, c in (x.split(":") for x in os.environ["SOAK_SHAPES"].split(","))]
 
 
 def soak(fam, k, m, cs, threads, seconds, slots):
