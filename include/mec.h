@@ -115,7 +115,7 @@ typedef struct {
     uint64_t queue_calls;        /* zero-copy calls served by the resident queue kernel */
     uint64_t queue_launches;     /* launches of the resident queue kernel (idle exits relaunch) */
     uint32_t queue_slots;        /* slots actually running (mec_set_host_queue may grant fewer) */
-    uint32_t queue_parts;        /* workgroups per slot (one per 16 KiB of chunk, at most 8) */
+    uint32_t queue_parts;        /* workgroups per slot (one per 16 KiB of chunk, at most 64) */
     uint32_t queue_broken;       /* 1: a call timed out and the queue stopped for good */
     uint32_t pad0;
     uint64_t queue_timeouts;     /* calls that hit MEC_QUEUE_TIMEOUT_MS */
@@ -285,18 +285,20 @@ int mec_set_coalescing(mec_ctx *ctx, uint32_t max_batch);
 
 /* Device-side submission queue for single-stripe host calls (queue.hip).
  * slots > 0 starts a resident kernel with `parts` workgroups per slot (one
- * per 16 KiB of chunk, at most 8; MEC_QUEUE_PARTS overrides), polling
+ * per 16 KiB of chunk, at most 64; MEC_QUEUE_PARTS overrides), polling
  * GPU-mapped host memory; mec_encode_host / mec_decode_host /
  * mec_encode_update_host calls of every family (RS and ISA-L byte-wise,
  * Jerasure Cauchy-RS as bitmatrix jobs) with chunks of at most
- * MEC_QUEUE_MAX_CHUNK bytes are then posted to a free slot instead of
+ * MEC_QUEUE_MAX_CHUNK bytes (default 1 MiB) are then posted to a free slot instead of
  * launching a kernel: no HIP runtime call on the caller's path (calls
  * beyond `slots` concurrent callers take the launch path).  Registered
  * chunks (mec_host_register) are coded in place; other host chunks are
  * copied through a mapped pinned staging buffer.
- * Slots: every workgroup must be resident at once, so `slots` is reduced to
- * what the device can hold (mec_stats.queue_slots reports the number
- * running; the call still returns MEC_OK).
+ * Slots: every workgroup must be resident at once, and the resident grid
+ * takes at most half of what the device can hold (launches beside it keep
+ * CUs), so `slots` is reduced to that (mec_stats.queue_slots reports the
+ * number running, e.g. 2 slots at 1 MiB chunks; the call still returns
+ * MEC_OK).
  * Idle: the kernel exits after MEC_QUEUE_IDLE_MS (default 50) without work
  * and is relaunched by the next call.
  * Timeout: a call not completed within MEC_QUEUE_TIMEOUT_MS (default 5000)

@@ -183,8 +183,8 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
     const uint64_t cb = uint64_t(p.chunk);
     const bool wave_ip = cb >= kBmWaveChunk || (R <= 2 && L.k >= 6 && cb >= (16u << 10) && cb <= (32u << 10));
     const uint32_t bt = L.stab ? gathered_block_threads(gshape)
-                               : block_threads(true, launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
-                                                                    int64_t(L.n_stripes) * L.dst_stripe_stride),
+                               : block_threads(true, bm_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
+                                                                int64_t(L.n_stripes) * L.dst_stripe_stride, cb, R, L.k),
                                                wave_ip);
     const Geometry g = geometry(L.packet / UB, bt);
     p.units = g.units;
@@ -217,7 +217,8 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
             } else {
                 p.src = L.src + int64_t(s0) * L.src_stripe_stride;
                 p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-                p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
+                p.win = bm_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride, cb, R,
+                                   L.k);
                 p.nstr = ns;
                 p.sgroup = stripe_group(p.chunk, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, true, p.srun);
                 const bool in_place = p.win > 1;
@@ -245,8 +246,9 @@ template <int W, int R>
 hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     if constexpr (bm_vw<W>() == 4) {
         if (!L.stab) {
-            const bool in_place = launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
-                                                 int64_t(L.n_stripes) * L.dst_stripe_stride) > 1;
+            const bool in_place = bm_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
+                                             int64_t(L.n_stripes) * L.dst_stripe_stride, L.packet * uint64_t(L.w), R,
+                                             L.k) > 1;
             if (bm_lane_bytes(W, R, L.packet * uint64_t(L.w), in_place) == 8) return run_bm_vw<W, R, 2>(L, stream);
         }
     }

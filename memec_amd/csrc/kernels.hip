@@ -264,6 +264,18 @@ uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int6
     const int64_t a1 = a0 + std::max<int64_t>(src_span, 0), b1 = b0 + std::max<int64_t>(dst_span, 0);
     return (b0 < a1 && a0 < b1) ? 2u : 1u;
 }
+uint32_t bm_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span, uint64_t chunk, int rows,
+                    int k) {
+    const uint32_t w = launch_windows(src, src_span, dst, dst_span);
+    if (w <= 1 || knob(kKnobWindows) != kKnobUnset) return w;
+    // tiny in-place stripes take the split-layout launch: identity order,
+    // one-wave blocks, split caps (tools/bm_small_ab.py MEC_WINDOWS=1 arm,
+    // profiles/r03/bm_small_win1_ab_{1,2}.log, two rounds): 1 KiB chunks
+    // +2-16 points for every (k, m) tried, 2 KiB with <= 2 outputs and
+    // k >= 8 +0.6-2.5; 2 KiB with 4 outputs or k <= 6 and 4 KiB lose 0.5-4
+    const bool tiny = chunk <= 1024 || (chunk <= 2048 && rows <= 2 && k >= 8);
+    return tiny ? 1u : w;
+}
 uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place) {
     // gathered (pointer-table) launches are instantiated for kThreads only
     if (!strided) return uint32_t(kThreads);

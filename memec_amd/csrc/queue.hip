@@ -33,8 +33,10 @@
 // grid to leave; if its job never ran, the caller codes it on the launch
 // path instead (queue_try returns false).
 //
-// Scope: chunks of at most MEC_QUEUE_MAX_CHUNK bytes (default 16 KiB;
-// larger chunks want the whole GPU, so they keep the launch path), either
+// Scope: chunks of at most MEC_QUEUE_MAX_CHUNK bytes (default 1 MiB: a
+// slot runs one workgroup per 16 KiB of chunk, at most kQMaxParts, and
+// measured faster than a launch from 4 KiB to 1 MiB for 1, 4 and 16
+// callers, profiles/r03/host/queue_fence_ab.jsonl, queue_cut_ab.jsonl), either
 // zero-copy (registered) or staged (mec.cpp lane_run), for every family:
 // byte-wise GF(2^8) products (RS, ISA-L) and the Jerasure Cauchy bitmatrix
 // over w packets of chunk/w bytes (cauchycoding.cc:80), whose masks the
@@ -272,13 +274,15 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
     for (;;) {
         if (t == 0 && part != 0) {  // the other parts: part 0's jobs, from device memory
             uint32_t c = 0;
-            // relaxed polls, one acquire fence per job taken: an acquire load
-            // per poll invalidated the L2 (buffer_inv) at every poll
+            // relaxed polls, one acquire fence per job taken (an acquire
+            // load per poll invalidated caches at every poll); system scope,
+            // as part 0's: this part reads the caller's chunks through its
+            // own XCD's L2, which must not serve lines of an earlier job
             for (;;) {
                 const uint64_t lf = __hip_atomic_load(left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t q = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (q > last) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                     last = q;
                     c = 1;
                     break;
@@ -437,7 +441,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     if (slots > kQMaxSlots) return fail(MEC_EINVAL, "at most %u queue slots", kQMaxSlots);
     DeviceGuard dg(c->device);
     std::unique_ptr<HostQueue> q(new HostQueue);
-    q->max_chunk = uint32_t(env_u64("MEC_QUEUE_MAX_CHUNK", 16 << 10));
+    q->max_chunk = uint32_t(env_u64("MEC_QUEUE_MAX_CHUNK", 1 << 20));
     // a lone call on a chunk above this codes faster as a launch (many
     // workgroups over PCIe) than on one queue workgroup
     q->solo_max = uint32_t(env_u64("MEC_QUEUE_SOLO_MAX", q->max_chunk));
@@ -454,13 +458,15 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     // idle threads only cost barrier time), at least 128 (descriptor loads)
     const uint32_t per_part = (units + q->parts - 1) / q->parts;
     q->threads = std::min<uint32_t>(kQThreads, std::max<uint32_t>(q->parts > 1 ? 64 : 128, (per_part + 63) / 64 * 64));
-    // every workgroup of every slot must be resident at once: a slot whose
-    // workgroup waits for another to exit would never be served
+    // every workgroup of every slot must be resident at once (a slot whose
+    // workgroup waits for another to exit would never be served), and the
+    // resident grid holds at most half of what the device can hold, so
+    // launches beside it (calls beyond the slots, batches) keep CUs to run on
     {
         int per_cu = 0, cus = 0;
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_kernel, int(q->threads), 0));
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-        const uint32_t cap = uint32_t(std::max(1, per_cu * cus)) / q->parts;
+        const uint32_t cap = uint32_t(std::max(1, per_cu * cus / 2)) / q->parts;
         slots = std::max<uint32_t>(1, std::min(slots, cap));
     }
     q->slots = slots;

@@ -138,6 +138,12 @@ uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool i
 // the input region's stripe span (one allocation, interleaved), else 1.
 // MEC_WINDOWS=<n> overrides (layout experiments).
 uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span);
+// Host: windows of a strided bitmatrix launch — launch_windows, except that
+// in-place launches of tiny stripes (chunks <= 1 KiB; <= 2 KiB with <= 2
+// outputs and k >= 8) run as split layouts do (1 window, which also picks
+// one-wave blocks and the split wave caps; kernels.hip).
+uint32_t bm_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span, uint64_t chunk, int rows,
+                    int k);
 
 // ---------------------------------------------------------------------------
 // partial (tail) units: < 16 bytes at the end of a region

@@ -87,12 +87,15 @@ def test_queue_cauchy_packet_tails(k, m, cs):
     _encode_decode_update("cauchy", k, m, cs)
 
 
-def _encode_decode_update(fam, k, m, cs, parts=1):
+def _encode_decode_update(fam, k, m, cs, parts=1, slots=8):
     slab = Slab(k + m + 1, cs, 31 + k)
     c = Codec(fam, k, m, cs)
     try:
         c.set_host_queue(8)
-        assert c.stats()["queue_parts"] == parts and c.stats()["queue_slots"] == 8
+        st = c.stats()
+        assert st["queue_parts"] == parts
+        # slots=None: capped by the device (at most half its resident 1024-thread workgroups)
+        assert st["queue_slots"] == slots if slots else 1 <= st["queue_slots"] * parts <= 128
         data = [slab.view(j).copy() for j in range(k)]
         want = O.encode(fam, k, m, [d.copy() for d in data], cs)
         q0 = c.stats()["queue_calls"]
@@ -154,6 +157,14 @@ def test_queue_multi_part_slots(fam, k, m, cs, qenv):
     word; partial units and bitmatrix packet tails land on the right part."""
     qenv(MEC_QUEUE_MAX_CHUNK=128 << 10)
     _encode_decode_update(fam, k, m, cs, parts=(cs // 16 + 1023) // 1024)
+
+
+@pytest.mark.parametrize("fam", ["rs", "cauchy"])
+def test_queue_default_cut_1mib(fam):
+    """The default chunk cut (1 MiB): 64 parts of 1024 threads per slot,
+    and the resident grid capped at half of what the device holds (256 CUs
+    x one 1024-thread workgroup -> 128 -> 2 slots of 64 parts)."""
+    _encode_decode_update(fam, 6, 3, 1 << 20, parts=64, slots=None)
 
 
 @pytest.mark.parametrize("pthr", [64, 256])
@@ -358,8 +369,8 @@ def test_queue_timeout_withdraws_and_falls_back(fam):
 def test_queue_fallbacks():
     """Calls the queue does not serve still code correctly through launches."""
     k, m = 4, 2
-    # chunk above MEC_QUEUE_MAX_CHUNK, then the queue stopped
-    cs = 128 << 10
+    # chunk above MEC_QUEUE_MAX_CHUNK (default 1 MiB), then the queue stopped
+    cs = (1 << 20) + 4096
     slab = Slab(k + m, cs, 4)
     c = Codec("rs", k, m, cs)
     try:
@@ -376,7 +387,7 @@ def test_queue_fallbacks():
         c.close()
         slab.close()
     # unregistered chunks above the queue's chunk limit: staged + launched
-    cs = 128 << 10
+    cs = (1 << 20) + 4096
     c = Codec("rs", k, m, cs)
     try:
         c.set_host_queue(4)
