@@ -171,3 +171,29 @@ def test_stripe_groups_default_rule_large_chunks(knobs):
     for s in (0, n - 1):
         assert np.array_equal(got[s], np.stack(O.encode("rs", k, m, [host[s, j].copy() for j in range(k)], cs)))
     c.close()
+
+
+@pytest.mark.parametrize("k,m,cs", [(8, 2, 2048), (12, 2, 2056), (12, 4, 1024), (4, 2, 520),  # tiny: split-layout launch
+                                    (6, 2, 2048), (12, 4, 2048), (8, 2, 4096)])                # other side of the rule
+def test_tiny_inplace_cauchy_rule(k, m, cs, knobs):
+    """In-place Cauchy-RS launches of tiny stripes run as split layouts
+    (bm_windows, kernels.hip: chunks <= 1 KiB, or <= 2 KiB with <= 2
+    outputs and k >= 8 -> one window, one-wave blocks, split caps): in-place
+    encode and decode of data + parity erasures on both sides of the rule,
+    and with the windows forced back to 2, equal the oracle."""
+    n = 40
+    base = _stripes_km("cauchy", k, m, cs, n, 1700 + k + cs)
+    c = Codec("cauchy", k, m, cs)
+    erased = sorted({0, k - 1, k + m - 1})[:m]
+    for win in (None, "2"):
+        knobs("MEC_WINDOWS", win)
+        st = torch.from_numpy(base.copy()).to("cuda")
+        st[:, k:] = 0
+        c.encode(st[:, :k], st[:, k:])
+        torch.cuda.synchronize()
+        assert np.array_equal(st.cpu().numpy(), base), ("in-place encode", k, m, cs, win)
+        st[:, erased] = 0
+        c.decode(st, sum(1 << i for i in range(k + m) if i not in erased))
+        torch.cuda.synchronize()
+        assert np.array_equal(st.cpu().numpy(), base), ("in-place decode", k, m, cs, win)
+    c.close()
