@@ -588,9 +588,9 @@ def load_traffic(cfg_name, stripes):
             j = json.load(f)
     except Exception as exc:
         return None, "unreadable PMC profile: %r" % exc
+    tag = j.get("round") or j.get("source", "").rpartition("tag ")[2] or "untagged"
     return j.get("hbm_bytes_per_launch"), ("profiles/pmc_%s.json (%s; rocprofv3 FETCH_SIZE + WRITE_SIZE passes, "
-                                          "gfx950-corrected; not measured in this run)"
-                                          % (cfg_name, j.get("round", "r02-final")))
+                                          "gfx950-corrected; not measured in this run)" % (cfg_name, tag))
 
 
 def launcher_cmd(argv, gpus, port, python=None):

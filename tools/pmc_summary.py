@@ -57,7 +57,7 @@ def main(cfgs, out_dir, tag):
             write_alg = (m if op == "encode" else len(erased)) * cs * stripes
         rd = 2 * fetch_kib * 1024
         wr = write_kib * 1024
-        rec = {"config": cfg, "kernels": names, "launches": [nf, nw],
+        rec = {"config": cfg, "round": tag, "kernels": names, "launches": [nf, nw],
                "FETCH_SIZE_kib_per_launch": fetch_kib, "WRITE_SIZE_kib_per_launch": write_kib,
                "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
                "hbm_bytes_per_launch": rd + wr,
