@@ -184,9 +184,7 @@ struct BmlParams {
     uint8_t mask[kMaxSrc][R * W];
 };
 
-// SST: the outputs go back through LDS too (each wave store 1 KiB of one
-// output chunk, as the loads) instead of straight from the lanes.
-template <int W, int R, bool SST>
+template <int W, int R>
 __global__ __launch_bounds__(256) void bml_kernel(const BmlParams<W, R> p) {
     constexpr int BT = 256, ROWS = R * W;
     __shared__ u32x4 buf[2][W * BT];  // [packet row x][lane]: S stripes' chunk, end to end
@@ -245,42 +243,17 @@ __global__ __launch_bounds__(256) void bml_kernel(const BmlParams<W, R> p) {
         load(A, j + 2);
         if (j + 1 < p.k) stage(B, j + 1);
     }
-    if constexpr (SST) {
-        // two output chunks per pass through the two LDS buffers
-        uint32_t ld[W];
+    const uint32_t so = cs * uint32_t(p.dss) + cu * 16;
 #pragma unroll
-        for (int x = 0; x < W; ++x) {
-            const uint32_t b = uint32_t(x) * kBmlBytes + t * 16, sl = b / C;
-            ld[x] = sl * uint32_t(p.dss) + (b - sl * C);
-        }
+    for (int i = 0; i < R; ++i)
 #pragma unroll
-        for (int i0 = 0; i0 < R; i0 += 2) {
-            __syncthreads();  // every lane is done with the LDS of the last pass
-#pragma unroll
-            for (int q = 0; q < 2 && i0 + q < R; ++q)
-#pragma unroll
-                for (int l = 0; l < W; ++l) buf[q][cbase + l * (P / 16)] = acc[(i0 + q) * W + l];
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < 2 && i0 + q < R; ++q)
-#pragma unroll
-                for (int x = 0; x < W; ++x) buf_st(buf[q][x * BT + t], dr, ld[x] + uint32_t(p.dst_off[i0 + q]));
-        }
-    } else {
-        const uint32_t so = cs * uint32_t(p.dss) + cu * 16;
-#pragma unroll
-        for (int i = 0; i < R; ++i)
-#pragma unroll
-            for (int l = 0; l < W; ++l) buf_st(acc[i * W + l], dr, so + uint32_t(p.dst_off[i]) + uint32_t(l) * P);
-    }
+        for (int l = 0; l < W; ++l) buf_st(acc[i * W + l], dr, so + uint32_t(p.dst_off[i]) + uint32_t(l) * P);
 }
 
 // Host: can this strided launch take bml_kernel?  In-place layouts
 // (outputs inside the inputs' stripe span), no accumulate, chunk a multiple
 // of 1 KiB, packet 256 B-4 KiB dividing 4096, stripe strides < 2 GiB / 16.
 bool bml_eligible(const BmLaunch &L);
-// ... and do its outputs go back through LDS (MEC_BM_LDS=2)?
-bool bml_staged_stores();
 
 template <int W, int R, int VW>
 hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
@@ -385,10 +358,7 @@ hipError_t run_bml(const BmLaunch &L, hipStream_t stream) {
     const uint32_t blocks = (L.n_stripes + S - 1) / S;
     if (blocks == 0) return hipSuccess;
     const uint32_t lds = occupancy_lds(256, 256, uint32_t(sizeof(u32x4)) * 2 * W * 256, bml_target_waves(R, W));
-    if (bml_staged_stores())
-        hipLaunchKernelGGL((bml_kernel<W, R, true>), dim3(blocks), dim3(256), lds, stream, p);
-    else
-        hipLaunchKernelGGL((bml_kernel<W, R, false>), dim3(blocks), dim3(256), lds, stream, p);
+    hipLaunchKernelGGL((bml_kernel<W, R>), dim3(blocks), dim3(256), lds, stream, p);
     return hipGetLastError();
 }
 

@@ -365,10 +365,8 @@ bool bml_eligible(const BmLaunch &L) {
     const bool in_place = launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
                                          int64_t(L.n_stripes) * L.dst_stripe_stride) > 1;
     if (!in_place) return false;
-    return e >= 1;  // default off until measured
+    return e == 1;  // default off until measured
 }
-
-bool bml_staged_stores() { return knob(kKnobBmLds) == 2; }
 
 uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32_t waves) {
     const int64_t e = knob(kKnobWpc);  // experiments (mec_set_knob)

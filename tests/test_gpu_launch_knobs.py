@@ -206,12 +206,11 @@ def test_lds_staged_bitmatrix_kernel(k, m, cs, n, knobs):
     through the LDS-staged kernel (MEC_BM_LDS=1) — S = 4096 / packet stripes
     per block with a partial last block (n not a multiple of S), w = 4, 8
     (k + m = 20 at 4 KiB) and 3 (3 KiB chunks), packets of 256 B-4 KiB —
-    equal the oracle, with the outputs stored from the lanes (1) or staged
-    through LDS too (2); MEC_BM_LDS=0 gives the same bytes through bm_kernel."""
+    equal the oracle; MEC_BM_LDS=0 gives the same bytes through bm_kernel."""
     base = _stripes_km("cauchy", k, m, cs, n, 2100 + k + cs)
     c = Codec("cauchy", k, m, cs)
     erased = sorted({0, k - 1, k + m - 1})[:m]
-    for lds in ("1", "2", "0"):
+    for lds in ("1", "0"):
         knobs("MEC_BM_LDS", lds)
         st = torch.from_numpy(base.copy()).to("cuda")
         st[:, k:] = 0
