@@ -156,105 +156,6 @@ __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
 
 hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream);
 
-// ---- LDS-staged variant for small in-place stripes (bml_kernel) ----------
-// With packets of 256 B-4 KiB a bm_kernel lane reads w slices a packet
-// apart, so each wave instruction covers 512 B of one packet; in place that
-// stream runs 70-74 % of 8 TB/s where the byte-wise pattern (every wave
-// instruction 1 KiB contiguous of one chunk) runs 76-79 %
-// (profiles/r02/xcd/bm_variants_v4.log).  Here a 256-thread block takes
-// S = 4096 / P stripes (P = packet bytes): every source chunk of its
-// stripes is read with the byte-wise pattern (round x of the block covers
-// bytes [4096 x, 4096 (x+1)) of the S chunks laid end to end, one 16-byte
-// unit per lane, 1 KiB contiguous per wave), staged in LDS (double buffer,
-// one barrier per chunk), and lane t then combines its 16-byte slice of
-// all w packets of stripe t / (P/16) from LDS with the same v_bitop3 masks
-// as bm_kernel.  The next chunk's loads are in flight while the current one
-// is combined.  Chunks must be multiples of 1 KiB (each wave's 1 KiB lies in
-// one chunk) and P must divide 4096 (bml_eligible).
-constexpr uint32_t kBmlBytes = 4096;  // bytes per block per packet row: 256 lanes x 16 B
-
-template <int W, int R>
-struct BmlParams {
-    const uint8_t *src;
-    uint8_t *dst;
-    int64_t sss, dss;
-    uint32_t chunk, packet, k, nstr;
-    int64_t src_off[kMaxSrc];
-    int64_t dst_off[R];
-    uint8_t mask[kMaxSrc][R * W];
-};
-
-template <int W, int R>
-__global__ __launch_bounds__(256) void bml_kernel(const BmlParams<W, R> p) {
-    constexpr int BT = 256, ROWS = R * W;
-    __shared__ u32x4 buf[2][W * BT];  // [packet row x][lane]: S stripes' chunk, end to end
-    const uint32_t t = threadIdx.x;
-    const uint32_t P = p.packet, C = p.chunk, S = kBmlBytes / P, U = P / 16;
-    const uint32_t s0 = blockIdx.x * S;
-    const uint32_t live = min(S, p.nstr - s0);  // stripes of this block that exist
-    // one resource per direction for the block's S stripes (out-of-range
-    // stripes of the last block: loads return 0, stores are dropped)
-    const __amdgpu_buffer_rsrc_t sr =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.src + int64_t(s0) * p.sss), 0,
-                                          int(uint32_t(live) * uint32_t(p.sss)), 0x00020000);
-    const __amdgpu_buffer_rsrc_t dr =
-        __builtin_amdgcn_make_buffer_rsrc(p.dst + int64_t(s0) * p.dss, 0, int(uint32_t(live) * uint32_t(p.dss)), 0x00020000);
-    // load mapping: round x, lane t -> byte b = 4096 x + 16 t of the block's
-    // chunk bytes -> stripe b / C, offset b % C
-    uint32_t lo[W];
-#pragma unroll
-    for (int x = 0; x < W; ++x) {
-        const uint32_t b = uint32_t(x) * kBmlBytes + t * 16, sl = b / C;
-        lo[x] = sl * uint32_t(p.sss) + (b - sl * C);
-    }
-    // compute mapping: lane t -> stripe t / U, 16-byte unit t % U of every packet
-    const uint32_t cs = t / U, cu = t - cs * U;
-    const uint32_t cbase = (cs * C) / 16 + cu;  // u32x4 index of packet 0's slice
-    u32x4 acc[ROWS];
-#pragma unroll
-    for (int r = 0; r < ROWS; ++r) acc[r] = u32x4{0, 0, 0, 0};
-    // Two register sets, A (even chunks) and B (odd), alternate without
-    // copies, and every load is unconditional (a chunk past k reads
-    // through a zero-record resource: no memory traffic, returns 0), so the
-    // compiler's wait before staging a chunk is exactly "all but the next
-    // chunk's W loads" on every path.
-    const __amdgpu_buffer_rsrc_t none = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p.src), 0, 0, 0x00020000);
-    auto load = [&](u32x4(&V)[W], uint32_t j) {
-        const __amdgpu_buffer_rsrc_t r = j < p.k ? sr : none;
-        const uint32_t so = j < p.k ? uint32_t(p.src_off[j]) : 0u;
-#pragma unroll
-        for (int x = 0; x < W; ++x) V[x] = buf_ld<u32x4>(r, lo[x] + so, true);
-    };
-    auto stage = [&](const u32x4(&V)[W], uint32_t j) {
-        u32x4 *L = buf[j & 1];
-#pragma unroll
-        for (int x = 0; x < W; ++x) L[x * BT + t] = V[x];
-        __syncthreads();
-        u32x4 d[W];
-#pragma unroll
-        for (int x = 0; x < W; ++x) d[x] = L[cbase + x * (P / 16)];
-        bm_combine<W, ROWS, u32x4>(d, acc, p.mask[j]);
-    };
-    u32x4 A[W], B[W];
-    load(A, 0);
-    for (uint32_t j = 0; j < p.k; j += 2) {
-        load(B, j + 1);
-        stage(A, j);
-        load(A, j + 2);
-        if (j + 1 < p.k) stage(B, j + 1);
-    }
-    const uint32_t so = cs * uint32_t(p.dss) + cu * 16;
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-#pragma unroll
-        for (int l = 0; l < W; ++l) buf_st(acc[i * W + l], dr, so + uint32_t(p.dst_off[i]) + uint32_t(l) * P);
-}
-
-// Host: can this strided launch take bml_kernel?  In-place layouts
-// (outputs inside the inputs' stripe span), no accumulate, chunk a multiple
-// of 1 KiB, packet 256 B-4 KiB dividing 4096, stripe strides < 2 GiB / 16.
-bool bml_eligible(const BmLaunch &L);
-
 template <int W, int R, int VW>
 hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
     constexpr int UB = 4 * VW;
@@ -339,34 +240,10 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
     return hipSuccess;
 }
 
-template <int W, int R>
-hipError_t run_bml(const BmLaunch &L, hipStream_t stream) {
-    BmlParams<W, R> p;
-    p.src = L.src;
-    p.dst = L.dst;
-    p.sss = L.src_stripe_stride;
-    p.dss = L.dst_stripe_stride;
-    p.packet = uint32_t(L.packet);
-    p.chunk = uint32_t(L.packet * uint64_t(L.w));
-    p.k = uint32_t(L.k);
-    p.nstr = L.n_stripes;
-    for (int j = 0; j < kMaxSrc; ++j) p.src_off[j] = j < L.k ? L.src_off[j] : 0;
-    for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
-    for (int j = 0; j < kMaxSrc; ++j)
-        for (int r = 0; r < R * W; ++r) p.mask[j][r] = j < L.k ? L.mask[j][r] : 0;
-    const uint32_t S = kBmlBytes / p.packet;
-    const uint32_t blocks = (L.n_stripes + S - 1) / S;
-    if (blocks == 0) return hipSuccess;
-    const uint32_t lds = occupancy_lds(256, 256, uint32_t(sizeof(u32x4)) * 2 * W * 256, bml_target_waves(R, W));
-    hipLaunchKernelGGL((bml_kernel<W, R>), dim3(blocks), dim3(256), lds, stream, p);
-    return hipGetLastError();
-}
-
 // Lane width of a strided launch (bm_lane_bytes); gathered launches keep
 // the default width.
 template <int W, int R>
 hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
-    if (bml_eligible(L)) return run_bml<W, R>(L, stream);
     if constexpr (bm_vw<W>() == 4) {
         if (!L.stab) {
             const bool in_place = bm_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,

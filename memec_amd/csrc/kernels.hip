@@ -346,28 +346,6 @@ uint32_t bm_target_waves(int rows, int w, int vw, bool in_place) {
     return in_place ? clampw(uint32_t(6 * rows), 6, 12) : clampw(uint32_t(6 * rows), 6, 16);
 }
 
-uint32_t bml_target_waves(int rows, int w) {
-    (void)rows;
-    (void)w;
-    return 0;
-}
-
-bool bml_eligible(const BmLaunch &L) {
-    const int64_t e = knob(kKnobBmLds);  // experiments (mec_set_knob)
-    if (e == 0) return false;
-    const uint64_t P = L.packet, C = P * uint64_t(L.w);
-    if (L.stab || L.accumulate || L.n_stripes == 0 || P < 256 || P > kBmlBytes || kBmlBytes % P || C % 1024) return false;
-    // buffer offsets: the S stripes of a block must fit a 32-bit record range
-    const uint64_t S = kBmlBytes / P;
-    if (L.src_stripe_stride <= 0 || L.dst_stripe_stride <= 0 || uint64_t(L.src_stripe_stride) * S >= (1ull << 31) ||
-        uint64_t(L.dst_stripe_stride) * S >= (1ull << 31))
-        return false;
-    const bool in_place = launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
-                                         int64_t(L.n_stripes) * L.dst_stripe_stride) > 1;
-    if (!in_place) return false;
-    return e == 1;  // default off until measured
-}
-
 uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32_t waves) {
     const int64_t e = knob(kKnobWpc);  // experiments (mec_set_knob)
     const bool forced = e != kKnobUnset;

@@ -22,7 +22,6 @@ enum Knob : int {
     kKnobBmVw,        // MEC_BM_VW=2|4
     kKnobWpc,         // MEC_WPC=<waves> (0 = no cap)
     kKnobCopyThreads, // MEC_COPY_THREADS=<n>
-    kKnobBmLds,       // MEC_BM_LDS=0|1 (LDS-staged bitmatrix kernel for small in-place stripes)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

@@ -248,9 +248,6 @@ uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accum
 // MEC_BM_VW=2|4 overrides (dwords per lane).
 uint32_t bm_lane_bytes(int w, int rows, uint64_t chunk, bool in_place);
 uint32_t bm_target_waves(int rows, int w, int vw, bool in_place);
-// Resident-wave target of bml_kernel (bm_kernel.hpp); 0 = no cap beyond its
-// static LDS (2 x w x 4 KiB per 4-wave block).
-uint32_t bml_target_waves(int rows, int w);
 // Dynamic LDS bytes per block of `bt` threads (`active` of them owning
 // units, `static_lds` bytes of static LDS) so that about `waves` active waves
 // share a CU; 0 = no cap.

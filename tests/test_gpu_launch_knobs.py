@@ -197,28 +197,3 @@ def test_tiny_inplace_cauchy_rule(k, m, cs, knobs):
         torch.cuda.synchronize()
         assert np.array_equal(st.cpu().numpy(), base), ("in-place decode", k, m, cs, win)
     c.close()
-
-
-@pytest.mark.parametrize("k,m,cs,n", [(12, 2, 2048, 37), (12, 2, 4096, 16), (8, 2, 16384, 5), (12, 4, 1024, 50),
-                                      (4, 2, 8192, 9), (16, 4, 4096, 11), (5, 2, 3072, 13), (1, 1, 1024, 17)])
-def test_lds_staged_bitmatrix_kernel(k, m, cs, n, knobs):
-    """bml_kernel (bm_kernel.hpp): in-place Cauchy-RS encode and decode
-    through the LDS-staged kernel (MEC_BM_LDS=1) — S = 4096 / packet stripes
-    per block with a partial last block (n not a multiple of S), w = 4, 8
-    (k + m = 20 at 4 KiB) and 3 (3 KiB chunks), packets of 256 B-4 KiB —
-    equal the oracle; MEC_BM_LDS=0 gives the same bytes through bm_kernel."""
-    base = _stripes_km("cauchy", k, m, cs, n, 2100 + k + cs)
-    c = Codec("cauchy", k, m, cs)
-    erased = sorted({0, k - 1, k + m - 1})[:m]
-    for lds in ("1", "0"):
-        knobs("MEC_BM_LDS", lds)
-        st = torch.from_numpy(base.copy()).to("cuda")
-        st[:, k:] = 0
-        c.encode(st[:, :k], st[:, k:])
-        torch.cuda.synchronize()
-        assert np.array_equal(st.cpu().numpy(), base), ("in-place encode", k, m, cs, lds)
-        st[:, erased] = 0
-        c.decode(st, sum(1 << i for i in range(k + m) if i not in erased))
-        torch.cuda.synchronize()
-        assert np.array_equal(st.cpu().numpy(), base), ("in-place decode", k, m, cs, lds)
-    c.close()

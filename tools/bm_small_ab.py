@@ -28,9 +28,9 @@ def env_list(name, default, conv=str):
 CASES = [(c.split(":")[0], int(c.split(":")[1]), int(c.split(":")[2]))
          for c in env_list("AB_CASES", ["cauchy:12:2", "cauchy:8:2", "cauchy:12:4"])]
 SIZES = env_list("AB_SIZES", [4096, 8192, 16384, 32768, 65536], int)
-# block:wpc[:vw[:windows[:lds]]] — MEC_BLOCK, MEC_WPC, MEC_BM_VW, MEC_WINDOWS, MEC_BM_LDS ("-" leaves a knob unset)
-KNOBS = ("MEC_BLOCK", "MEC_WPC", "MEC_BM_VW", "MEC_WINDOWS", "MEC_BM_LDS")
-ARMS = [tuple((a + ":-:-:-:-").split(":")[:5])
+# block:wpc[:vw[:windows]] — MEC_BLOCK, MEC_WPC, MEC_BM_VW, MEC_WINDOWS ("-" leaves a knob unset)
+KNOBS = ("MEC_BLOCK", "MEC_WPC", "MEC_BM_VW", "MEC_WINDOWS")
+ARMS = [tuple((a + ":-:-:-").split(":")[:4])
         for a in env_list("AB_ARMS", ["-:-", "64:0", "64:8", "64:12", "64:16", "256:0", "256:8", "256:12", "256:16"])]
 OPS = env_list("AB_OPS", ["enc_split", "enc_inplace", "dec_inplace"])
 
