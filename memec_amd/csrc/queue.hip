@@ -7,15 +7,18 @@
 // thread, takes runtime locks shared by every caller, and completion is
 // seen through hipStreamSynchronize.  This queue removes the runtime from
 // the per-call path:
-//   * a resident kernel runs one workgroup per slot; each polls its slot in
-//     GPU-mapped, coherent host memory (system-scope acquire loads);
+//   * a resident kernel runs `parts` workgroups per slot (one per 16 KiB of
+//     chunk); part 0 polls its slot in GPU-mapped, coherent host memory
+//     (relaxed system-scope loads, one acquire per job taken) and hands
+//     each job to the other parts through device memory;
 //   * a caller takes a free slot, writes the call's descriptor (device
 //     addresses of registered chunks, GF(2^8) coefficients), publishes a new
-//     sequence number, and spins on the slot's `done` word, which the
-//     workgroup stores (system-scope release) after its outputs;
-//   * the workgroup builds the v_perm tables (gf8_kernel.hpp) from the raw
-//     coefficients in LDS and codes the chunk over PCIe, one 16-byte unit
-//     per lane.
+//     sequence number, and spins on the slot's `done` words, which every
+//     part stores (system-scope release, one L2 writeback) after its
+//     outputs;
+//   * each part builds the v_perm tables (gf8_kernel.hpp) from the raw
+//     coefficients in LDS and codes its share of the chunk over PCIe, one
+//     16-byte unit per lane.
 // Exit conditions every wave reaches: the stop word (mec_set_host_queue(0),
 // mec_destroy, a timed-out call) or a grid-wide idle exit.  The idle exit is
 // decided for the whole grid at once: workgroup 0 (the leader) watches every
