@@ -19,7 +19,7 @@ import bench  # noqa: E402
 from cap_ab import workload  # noqa: E402
 from memec_amd import set_knob  # noqa: E402
 
-KNOBS = ("MEC_BLOCK", "MEC_WINDOWS", "MEC_WPC", "MEC_BM_VW")
+KNOBS = ("MEC_BLOCK", "MEC_WINDOWS", "MEC_WPC", "MEC_BM_VW", "MEC_UPT")
 
 
 def parse_arms(text):
