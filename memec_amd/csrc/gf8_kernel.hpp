@@ -137,9 +137,6 @@ __device__ __forceinline__ void gf8_apply(const u32x4 (&d)[K], u32x4 (&acc)[R], 
         if (has[i]) acc[i] ^= pend[i];
 }
 
-// Host: units per lane of in-place dense launches (MEC_UPT; 1 unless set).
-int gf8_upt();
-
 // Host side: the structure a coefficient block qualifies for.
 inline int gf8_structure(const Gf8Coef (*coef)[kMaxSrc], int k, int rows) {
     const uint32_t one = 0x03020100u;  // t0 of coefficient 1 (identity on bits 0-2)
@@ -153,14 +150,7 @@ inline int gf8_structure(const Gf8Coef (*coef)[kMaxSrc], int k, int rows) {
 // caller's Chunk* arrays) instead of base + stripe * stride + offset; the
 // map stays in kernel arguments, so a block's only extra latency is one
 // batch of scalar loads of its pointers.
-// UPT: 16-byte units per lane.  UPT = 2 gives each lane units u and
-// u + BT (a block covers 2 BT units of a stripe): all 2K source loads of
-// the lane are issued before the first is combined, so a wave keeps twice
-// the bytes in flight (an experiment for the in-place decodes, whose
-// memory-side reads in flight run 13 % under the split encode's; DESIGN
-// §9).  Units past the chunk read 0 and drop their stores (the chunk's
-// buffer resource ends at the chunk).
-template <int K, int R, bool G, int S, int BT, int UPT = 1>
+template <int K, int R, bool G, int S, int BT>
 __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     __shared__ uint32_t tab[R * K * 8];
     for (int t = threadIdx.x; t < R * K; t += BT) {
@@ -175,13 +165,14 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     const uint32_t bid = block_order(p.win);
     uint32_t stripe, tile;
     stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, stripe, tile);
-    const uint32_t u = tile * BT * UPT + threadIdx.x;
+    const uint32_t u = tile * BT + threadIdx.x;
     if (u >= p.units) return;
     // Every chunk is a buffer resource (SGPR base, 32-bit lane offsets) in
     // both modes: strided chunk bases are uniform per block too, and the
     // same non-temporal stream runs 2-3 points faster through buffer
     // instructions than through 64-bit flat addresses at the product's
     // wave caps (tools/policy_probe.hip, profiles/r02/policy/).
+    const uint32_t off = u * 16;
     // chunk addresses (uniform): source j / output i of this stripe
     const uint64_t gs = p.s0 + stripe;
     auto src_at = [&](int j) -> uint64_t {
@@ -192,46 +183,20 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
         if constexpr (G) return p.dtab[gs * p.dstride + p.dst_off[i]];
         else return uint64_t(uintptr_t(p.dst + int64_t(stripe) * p.dss + p.dst_off[i]));
     };
-    if constexpr (UPT == 1) {
-        const uint32_t off = u * 16;
-        u32x4 d[K];
+    u32x4 d[K];
 #pragma unroll
-        for (int j = 0; j < K; ++j) d[j] = buf_ld<u32x4>(chunk_rsrc(src_at(j), p.chunk), off, true);
-        __amdgpu_buffer_rsrc_t dr[R];
+    for (int j = 0; j < K; ++j) d[j] = buf_ld<u32x4>(chunk_rsrc(src_at(j), p.chunk), off, true);
+    __amdgpu_buffer_rsrc_t dr[R];
 #pragma unroll
-        for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(dst_at(i), p.chunk);
-        u32x4 acc[R];
-        // read-modify-write of the outputs (delta updates) is streamed too
-        // (non-temporal: RS(10,4) update 70.9 -> 73.9 %)
+    for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(dst_at(i), p.chunk);
+    u32x4 acc[R];
+    // read-modify-write of the outputs (delta updates) is streamed too
+    // (non-temporal: RS(10,4) update 70.9 -> 73.9 %)
 #pragma unroll
-        for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
-        gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
+    for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
+    gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
 #pragma unroll
-        for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
-    } else {
-        u32x4 d[UPT][K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) {
-            const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(src_at(j), p.chunk);
-#pragma unroll
-            for (int q = 0; q < UPT; ++q) d[q][j] = buf_ld<u32x4>(sr, (u + q * BT) * 16, true);
-        }
-        __amdgpu_buffer_rsrc_t dr[R];
-#pragma unroll
-        for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(dst_at(i), p.chunk);
-        u32x4 acc[UPT][R];
-#pragma unroll
-        for (int q = 0; q < UPT; ++q)
-#pragma unroll
-            for (int i = 0; i < R; ++i)
-                acc[q][i] = p.accumulate ? buf_ld<u32x4>(dr[i], (u + q * BT) * 16, true) : u32x4{0, 0, 0, 0};
-#pragma unroll
-        for (int q = 0; q < UPT; ++q) {
-            gf8_apply<K, R, S>(d[q], acc[q], tab + opaque_zero());
-#pragma unroll
-            for (int i = 0; i < R; ++i) buf_st(acc[q][i], dr[i], (u + q * BT) * 16);
-        }
-    }
+    for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
 }
 
 // The < 16-byte remainder of each region (chunk sizes that are not a
@@ -275,12 +240,7 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                                : block_threads(true, launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
                                                                     int64_t(L.n_stripes) * L.dst_stripe_stride),
                                                wave_ok);
-    // units per lane (experiment knob MEC_UPT=2: in-place dense launches
-    // with 256-thread blocks only)
-    const bool upt2 = !L.stab && !L.probe && bt == kThreads && gf8_structure(L.coef, K, R) != kGf8Vand && gf8_upt() == 2 &&
-                      launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
-                                     int64_t(L.n_stripes) * L.dst_stripe_stride) > 1;
-    const Geometry g = geometry(L.len / 16, bt * (upt2 ? 2 : 1));
+    const Geometry g = geometry(L.len / 16, bt);
     p.units = g.units;
     p.tiles = g.tiles;
     p.accumulate = L.accumulate ? 1u : 0u;
@@ -337,8 +297,6 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                 } else {
                     if (vand)
                         hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand, kThreads>), grid, block, lds, stream, p);
-                    else if (upt2)
-                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Dense, kThreads, 2>), grid, block, lds, stream, p);
                     else
                         hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Dense, kThreads>), grid, block, lds, stream, p);
                 }

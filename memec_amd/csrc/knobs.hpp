@@ -22,7 +22,6 @@ enum Knob : int {
     kKnobBmVw,        // MEC_BM_VW=2|4
     kKnobWpc,         // MEC_WPC=<waves> (0 = no cap)
     kKnobCopyThreads, // MEC_COPY_THREADS=<n>
-    kKnobUpt,         // MEC_UPT=1|2 (16-byte units per lane of in-place dense gf8 launches)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

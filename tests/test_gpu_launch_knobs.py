@@ -197,15 +197,3 @@ def test_tiny_inplace_cauchy_rule(k, m, cs, knobs):
         torch.cuda.synchronize()
         assert np.array_equal(st.cpu().numpy(), base), ("in-place decode", k, m, cs, win)
     c.close()
-
-
-@pytest.mark.parametrize("fam", ["rs", "isal_rs", "isal_cauchy"])
-@pytest.mark.parametrize("cs", [4096, 4128, 65536 + 2048])
-def test_two_units_per_lane(fam, cs, knobs):
-    """MEC_UPT=2: in-place dense (decode) launches with 256-thread blocks
-    give each lane units u and u + 256; partial last tiles (units past the
-    chunk read 0 and drop their stores through the chunk's buffer
-    resource) and tails stay bit-exact in every layout."""
-    knobs("MEC_UPT", "2")
-    knobs("MEC_BLOCK", "256")
-    _check_all_layouts(fam, cs, 2300 + cs)

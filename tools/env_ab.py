@@ -19,7 +19,7 @@ import bench  # noqa: E402
 from cap_ab import workload  # noqa: E402
 from memec_amd import set_knob  # noqa: E402
 
-KNOBS = ("MEC_BLOCK", "MEC_WINDOWS", "MEC_WPC", "MEC_BM_VW", "MEC_UPT")
+KNOBS = ("MEC_BLOCK", "MEC_WINDOWS", "MEC_WPC", "MEC_BM_VW")
 
 
 def parse_arms(text):
