@@ -1072,8 +1072,10 @@ def main():
                                               "shape, so frac_of_xor_twin ~1 says the arithmetic costs nothing; it "
                                               "is not an upper bound (the arithmetic shifts wave timing, and the "
                                               "coding kernel may run up to a few % faster). region_xor_2r1w = "
-                                              "mec_xor over 3 x 8 GiB (2 reads + 1 write per lane): the fastest "
-                                              "read/write stream libmec runs on this box, the ceiling to compare with"},
+                                              "mec_xor over 3 x 8 GiB (2 reads + 1 write per lane), a second live "
+                                              "read/write stream for box-to-box comparison; the coding kernel runs "
+                                              "0.96-1.04x of it, so neither is a hard bound: the bound is "
+                                              "peak (spec HBM3E)"},
             "parity": parity_pin,
             "cpu_baseline": None,
         }
