@@ -24,6 +24,8 @@ def main():
     gib = float(sys.argv[7]) if len(sys.argv) > 7 else 8
     n = max(1, int(gib * (1 << 30)) // ((k + m) * cs))
     c = Codec(fam, k, m, cs)
+    if os.environ.get("SHAPE_TWIN") == "1":  # the launch's XOR-only twin (mec_set_probe)
+        c.set_probe(True)
     if op == "enc_split":
         data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
         fill_random(data, 1)
@@ -47,8 +49,8 @@ def main():
         ev[1].synchronize()
         ms.append(ev[0].elapsed_time(ev[1]))
     nbytes = (k + m) * cs * n
-    print("%s %d %d %d %s n=%d best %.4f ms %.2f %%" % (fam, k, m, cs, op, n, min(ms), nbytes / (min(ms) * 1e-3) / 8e12 * 100),
-          flush=True)
+    print("%s %d %d %d %s%s n=%d best %.4f ms %.2f %%" % (fam, k, m, cs, op, " twin" if os.environ.get("SHAPE_TWIN") == "1" else "",
+                                                         n, min(ms), nbytes / (min(ms) * 1e-3) / 8e12 * 100), flush=True)
 
 
 if __name__ == "__main__":
