@@ -245,6 +245,53 @@ def cpu_baseline_reference(fam, k, m, cs, gpu_parity_np, seed, threads, op, eras
             "cpu_model": cpu_model()}
 
 
+def configs0_reference(seconds=2.0):
+    """BASELINE configs[0] as it is quoted: RS(4,2) encode and decode of
+    erasures {0,1} at 4 KiB chunks through the reference's own CPU path
+    (oracle/_ref: MemEC's Coding + Jerasure + gf_complete compiled from its
+    sources), one process, one thread, as performance.cc runs it; about
+    `seconds` of timed work per leg.  The decode's output is checked against
+    the codewords and the encode's against the oracle."""
+    L = _ref_lib()
+    if L is None:
+        return None
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    k, m, cs, n = 4, 2, 4096, 256
+    h = L.ref_instantiate(4, k, m, cs)  # CS_RS
+    if not h:
+        return None
+    try:
+        data = O.fill(n * k * cs, 0x4D454D4543)
+        par = np.zeros(n * m * cs, np.uint8)
+        probe = L.ref_encode_batch_mt(h, data.ctypes.data, par.ctypes.data, n, 1, 1)
+        ep = max(1, int(seconds / max(probe, 1e-6)))
+        log("configs[0]: reference RS(4,2)@4 KiB encode, %d stripes x %d passes on 1 thread" % (n, ep))
+        et = L.ref_encode_batch_mt(h, data.ctypes.data, par.ctypes.data, n, 1, ep)
+        enc_ok = all(np.array_equal(par[s_ * m * cs:(s_ + 1) * m * cs],
+                                    np.stack(O.encode("rs", k, m, [data[(s_ * k + j) * cs:(s_ * k + j + 1) * cs].copy()
+                                                                   for j in range(k)], cs)).reshape(-1))
+                     for s_ in (0, n - 1))
+        code = np.concatenate([data.reshape(n, k, cs), par.reshape(n, m, cs)], axis=1)
+        buf = code.reshape(-1).copy()
+        present = 0b111100
+        probe = L.ref_decode_batch_mt(h, buf.ctypes.data, n, present, 1, 1)
+        dp = max(1, int(seconds / max(probe, 1e-6)))
+        log("configs[0]: reference RS(4,2)@4 KiB decode {0,1}, %d stripes x %d passes on 1 thread" % (n, dp))
+        dt = L.ref_decode_batch_mt(h, buf.ctypes.data, n, present, 1, dp)
+        dec_ok = dt > 0 and bool(np.array_equal(buf.reshape(n, k + m, cs), code))
+    finally:
+        L.ref_destroy(h)
+    return {"kind": "reference", "unit": "GiB/s", "cores": 1,
+            "encode_value": round(ep * n * k * cs / et / 2**30, 4),
+            "decode_value": round(dp * n * k * cs / dt / 2**30, 4) if dt > 0 else None,
+            "sample": "%d stripes x %d / %d passes through MemEC's own Coding::encode(index 1) / Coding::decode "
+                      "(erasures {0,1}), compiled from the reference sources (oracle/_ref), one thread, as "
+                      "performance.cc" % (n, ep, dp),
+            "encode_matches_oracle": bool(enc_ok), "decode_restores_codewords": dec_ok, "cpu_model": cpu_model()}
+
+
 def cpu_baseline_reference_update(fam, k, m, cs, j, threads):
     """kind "reference" for the delta path: MemEC's own calls as each parity
     server makes them (parity_chunk_buffer.cc:342-353, 387-393) — per
@@ -663,7 +710,9 @@ def probe_warmup(step, sync):
 # command record every GPU config north_star asks for: configs[3] at its
 # per-GPU batch (weak) and configs[4] encode + decode as the fixed global
 # batch of 32768 stripes sharded over the ranks (strong), as BASELINE states.
-EXTRA_CONFIGS = (("configs[3]", "rs8_small", None), ("configs[4]", "crs_enc", 32768))
+EXTRA_CONFIGS = (("configs[0]", "rs42", None), ("configs[3]", "rs8_small", None), ("configs[4]", "crs_enc", 32768))
+# encode configs whose decode twin is timed too (the others verify a decode untimed)
+DECODE_TWINS = {"crs_enc": "crs_dec", "rs42": "rs42_dec"}
 
 
 def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_ok):
@@ -708,7 +757,7 @@ def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_
     enc_step = lambda: codec.encode(data, parity)  # noqa: E731
     res.update(run(enc_step, (k + m) * cs * stripes))
     res["parity"] = pin(check_encode(fam, k, m, cs, data, parity))
-    twin = {"crs_enc": "crs_dec"}.get(name)
+    twin = DECODE_TWINS.get(name)
     erased = CONFIGS[twin][6] if twin else list(range(m))
     n = stripes if twin else min(stripes, 4096)
     st = torch.empty(n, k + m, cs, dtype=torch.uint8, device=dev)
@@ -721,7 +770,7 @@ def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_
     dec_step = lambda: codec.decode(st, present)  # noqa: E731
     if twin:
         dec = run(dec_step, (k + len(erased)) * cs * n)
-        dec["workload"] = workload_name(twin, n, True, global_stripes)
+        dec["workload"] = workload_name(twin, n, bool(strong_global), global_stripes)
         dec["erased"] = erased
     else:
         dec_step()
@@ -1088,6 +1137,12 @@ def main():
             line["e2e_host_memory"] = e2e
         if extras:
             line["other_configs"] = extras
+            if "configs[0]" in extras and world == 1 and not args.no_cpu_baseline:
+                # configs[0] is the reference's own CPU path: time it here too
+                try:
+                    extras["configs[0]"]["reference_cpu"] = configs0_reference()
+                except Exception as exc:  # report, never fake
+                    extras["configs[0]"]["reference_cpu"] = {"error": repr(exc)}
         if secondary:
             line["decode"] = secondary
         if not args.no_cpu_baseline and world == 1:

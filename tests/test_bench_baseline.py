@@ -173,3 +173,15 @@ def test_spread_indices():
     assert bench.spread(3, 3, 4) == []
     assert bench.spread(0, 4096, 13)[0] == 0 and bench.spread(0, 4096, 13)[-1] == 4095
     assert len(bench.spread(0, 4096, 13)) == 13 and len(bench.spread(0, 5, 13)) == 5
+
+
+def test_configs0_reference_cpu_leg():
+    """BASELINE configs[0] through the reference's own CPU path
+    (oracle/_ref): RS(4,2)@4 KiB encode and decode {0,1} on one thread,
+    outputs checked (encode vs the oracle, decode vs the codewords)."""
+    if bench._ref_lib() is None:
+        pytest.skip("oracle/_ref not built here")
+    r = bench.configs0_reference(seconds=0.05)
+    assert r["kind"] == "reference" and r["cores"] == 1
+    assert r["encode_value"] > 0 and r["decode_value"] > 0
+    assert r["encode_matches_oracle"] is True and r["decode_restores_codewords"] is True

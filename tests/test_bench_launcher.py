@@ -73,10 +73,17 @@ def test_host_cores():
 
 
 def test_extra_configs_are_baseline_configs():
-    """The default line's other_configs: configs[3] per GPU (weak) and
-    configs[4] as BASELINE's 32768-stripe global batch sharded over ranks."""
+    """The default line's other_configs: configs[0]'s RS(4,2)@4 KiB shape on
+    the GPU per GPU (weak, encode + timed decode {0,1}), configs[3] per GPU
+    (weak) and configs[4] as BASELINE's 32768-stripe global batch sharded
+    over ranks."""
     labels = {label: (name, strong) for label, name, strong in bench.EXTRA_CONFIGS}
-    assert labels == {"configs[3]": ("rs8_small", None), "configs[4]": ("crs_enc", 32768)}
+    assert labels == {"configs[0]": ("rs42", None), "configs[3]": ("rs8_small", None),
+                      "configs[4]": ("crs_enc", 32768)}
+    assert bench.DECODE_TWINS == {"crs_enc": "crs_dec", "rs42": "rs42_dec"}
+    fam, k, m, cs, stripes, op, _ = bench.CONFIGS["rs42"]
+    assert (fam, k, m, cs, op) == ("rs", 4, 2, 4096, "encode") and bench.CONFIGS["rs42_dec"][6] == [0, 1]
+    assert "stripes total" not in bench.workload_name("rs42_dec", 65536, False, 65536)
     fam, k, m, cs, stripes, op, _ = bench.CONFIGS["rs8_small"]
     assert (fam, k, m, cs, stripes, op) == ("rs", 8, 2, 4096, 65536, "encode")
     fam, k, m, cs, stripes, op, _ = bench.CONFIGS["crs_enc"]

@@ -48,6 +48,10 @@ def test_bench_gpus2_default_line_rehearsal():
     assert rec["parity"]["equal"] is True and rec["parity"]["ranks"] == 2
     assert rec["decode"]["verified"] is True and rec["decode"]["parity"]["equal"] is True
     assert rec["decode"]["parity"]["non_codeword_stripes"] > 0
+    c0 = rec["other_configs"]["configs[0]"]
+    assert c0["stripes_per_gpu"] == 65536 and c0["global_stripes"] == 131072 and c0["parity"]["equal"] is True
+    assert c0["decode"]["verified"] is True and c0["decode"]["parity"]["equal"] is True
+    assert "reference_cpu" not in c0  # the CPU leg runs at N = 1 only
     c3, c4 = rec["other_configs"]["configs[3]"], rec["other_configs"]["configs[4]"]
     assert c3["stripes_per_gpu"] == 65536 and c3["global_stripes"] == 131072
     assert c3["verified"] is True and c3["parity"]["equal"] is True and c3["decode_parity"]["equal"] is True
