@@ -49,8 +49,7 @@ struct BmParams {
     uint32_t sstride, dstride, chunk, s0;
     uint64_t packet;
     uint32_t units, tiles, k, accumulate, win, pad;
-    uint32_t nstr, sgroup, srun;  // stripe-group map (stream_common.hpp stripe_tile)
-    uint32_t rot;                 // strided: stripe s reads its sources from (s mod k) on (bm_rotate)
+    uint32_t nstr, sgroup, srun, pad2;  // stripe-group map (stream_common.hpp stripe_tile)
     int64_t src_off[kMaxSrc];
     int64_t dst_off[R];
     uint8_t mask[kMaxSrc][R * W];
@@ -126,10 +125,6 @@ __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
         const uint32_t pk = uint32_t(p.packet);
         const uint8_t *sb = p.src + int64_t(stripe) * p.sss;
         uint8_t *db = p.dst + int64_t(stripe) * p.dss;
-        // source order: 0, 1, ... or rotated to start at stripe mod k, so
-        // waves of neighbouring stripes stream different chunks at once
-        const uint32_t r0 = p.rot ? stripe % p.k : 0u;
-        auto at = [&](uint32_t j) { return j + r0 < p.k ? j + r0 : j + r0 - p.k; };
         __amdgpu_buffer_rsrc_t dr[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(uint64_t(uintptr_t(db + p.dst_off[i])), p.chunk);
@@ -138,17 +133,17 @@ __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
 #pragma unroll
             for (int l = 0; l < W; ++l) acc[i * W + l] = p.accumulate ? buf_ld<vec>(dr[i], off + l * pk, true) : vec(0);
         {
-            const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(uint64_t(uintptr_t(sb + p.src_off[at(0)])), p.chunk);
+            const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(uint64_t(uintptr_t(sb + p.src_off[0])), p.chunk);
 #pragma unroll
             for (int x = 0; x < W; ++x) d[x] = buf_ld<vec>(sr, off + x * pk, true);
         }
         for (uint32_t j = 0; j < p.k; ++j) {
             if (j + 1 < p.k) {
-                const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(uint64_t(uintptr_t(sb + p.src_off[at(j + 1)])), p.chunk);
+                const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(uint64_t(uintptr_t(sb + p.src_off[j + 1])), p.chunk);
 #pragma unroll
                 for (int x = 0; x < W; ++x) nx[x] = buf_ld<vec>(sr, off + x * pk, true);
             }
-            bm_combine<W, ROWS, vec>(d, acc, p.mask[at(j)]);
+            bm_combine<W, ROWS, vec>(d, acc, p.mask[j]);
 #pragma unroll
             for (int x = 0; x < W; ++x) d[x] = nx[x];
         }
@@ -200,7 +195,7 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
     p.nstr = 0;
     p.sgroup = 0;
     p.srun = 8;
-    p.rot = bm_rotate() ? 1u : 0u;
+    p.pad2 = 0;
     for (int j = 0; j < kMaxSrc; ++j) p.src_off[j] = j < L.k ? L.src_off[j] : 0;
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int j = 0; j < kMaxSrc; ++j)

@@ -346,8 +346,6 @@ uint32_t bm_target_waves(int rows, int w, int vw, bool in_place) {
     return in_place ? clampw(uint32_t(6 * rows), 6, 12) : clampw(uint32_t(6 * rows), 6, 16);
 }
 
-bool bm_rotate() { return knob(kKnobBmRot) == 1; }
-
 uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32_t waves) {
     const int64_t e = knob(kKnobWpc);  // experiments (mec_set_knob)
     const bool forced = e != kKnobUnset;

@@ -22,7 +22,6 @@ enum Knob : int {
     kKnobBmVw,        // MEC_BM_VW=2|4
     kKnobWpc,         // MEC_WPC=<waves> (0 = no cap)
     kKnobCopyThreads, // MEC_COPY_THREADS=<n>
-    kKnobBmRot,       // MEC_BM_ROT=0|1 (rotated source order per stripe, strided bitmatrix launches)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

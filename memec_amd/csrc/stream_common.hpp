@@ -248,9 +248,6 @@ uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accum
 // MEC_BM_VW=2|4 overrides (dwords per lane).
 uint32_t bm_lane_bytes(int w, int rows, uint64_t chunk, bool in_place);
 uint32_t bm_target_waves(int rows, int w, int vw, bool in_place);
-// Strided bitmatrix launches: rotate each stripe's source order to start at
-// stripe mod k (MEC_BM_ROT=1; off unless set).
-bool bm_rotate();
 // Dynamic LDS bytes per block of `bt` threads (`active` of them owning
 // units, `static_lds` bytes of static LDS) so that about `waves` active waves
 // share a CU; 0 = no cap.

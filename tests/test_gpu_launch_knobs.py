@@ -197,11 +197,3 @@ def test_tiny_inplace_cauchy_rule(k, m, cs, knobs):
         torch.cuda.synchronize()
         assert np.array_equal(st.cpu().numpy(), base), ("in-place decode", k, m, cs, win)
     c.close()
-
-
-@pytest.mark.parametrize("cs", [96, 4096, 65536])
-def test_bitmatrix_rotated_source_order(cs, knobs):
-    """MEC_BM_ROT=1: strided bitmatrix launches read each stripe's sources
-    starting at stripe mod k (XOR order only) — every layout bit-exact."""
-    knobs("MEC_BM_ROT", "1")
-    _check_all_layouts("cauchy", cs, 2500 + cs)
