@@ -24,7 +24,7 @@ from memec_amd import Codec, fill_random, set_knob  # noqa: E402
 CASES = [("rs", 10, 4, 1 << 20, 4096, [0, 1, 2, 3]), ("cauchy", 12, 4, 65536, 32768, [0, 1, 2, 3])]
 # arms: label -> knobs (MEC_WINDOWS / MEC_SGROUP through mec_set_knob)
 ARMS = {"win2": {"MEC_WINDOWS": "2"}, "win4": {"MEC_WINDOWS": "4"}, "perm": {"MEC_SGROUP": "p"},
-        "default": {}, "rot": {"MEC_BM_ROT": "1"}}
+        "default": {}}
 if os.environ.get("PLACE_ARMS"):
     ARMS = {a: ARMS[a] for a in os.environ["PLACE_ARMS"].split(",")}
 
@@ -46,7 +46,7 @@ def main():
             res = {w: [] for w in wins}
             for _ in range(3):
                 for w in wins:
-                    for kn in ("MEC_WINDOWS", "MEC_SGROUP", "MEC_BM_ROT"):
+                    for kn in ("MEC_WINDOWS", "MEC_SGROUP"):
                         set_knob(kn, ARMS[w].get(kn))
                     c.decode(st, present)
                     best = None
@@ -58,7 +58,7 @@ def main():
                         ms = ev[0].elapsed_time(ev[1])
                         best = ms if best is None else min(best, ms)
                     res[w].append(best)
-            for kn in ("MEC_WINDOWS", "MEC_SGROUP", "MEC_BM_ROT"):
+            for kn in ("MEC_WINDOWS", "MEC_SGROUP"):
                 set_knob(kn, None)
             pct = {w: nbytes / (statistics.median(v) * 1e-3) / 8e12 * 100 for w, v in res.items()}
             print("%-6s k=%-2d cs=%-7d n=%-5d offset %5.1f GiB (st at %#x)  " % (fam, k, cs, n, d, st.data_ptr()) +
