@@ -8,6 +8,7 @@ The fixed cases in test_gpu_parity.py pin the BASELINE shapes; this sweep
 covers the row-group splits of the kernels (m > 4 parities, decode of > 4
 erasures, k up to 31) and chunk sizes that are not multiples of 16 B.
 """
+import os
 import random
 
 import numpy as np
@@ -33,14 +34,14 @@ def _gpu():
     torch.cuda.synchronize()
 
 
-def _shapes(fam, count, seed):
+def _shapes(fam, count, seed, max_units=96):
     rng = random.Random(seed)
     out = []
     while len(out) < count:
         n_total = rng.randint(2, 32)
         m = rng.randint(1, n_total - 1)
         k = n_total - m
-        cs = 8 * rng.randint(1, 96)  # 8 .. 768 B: tails below 16 B included
+        cs = 8 * rng.randint(1, max_units)  # 8 .. 768 B by default: tails below 16 B included
         if fam == "cauchy":
             w = O.cauchy_getw(k, m, cs)
             if w < 1 or w > 8:
@@ -51,9 +52,22 @@ def _shapes(fam, count, seed):
 
 @pytest.mark.parametrize("fam", FAMS)
 def test_geometry_sweep_vs_oracle(fam):
-    rng = random.Random(0x5EED + FAMS.index(fam))
-    n = 2
-    for (k, m, cs) in _shapes(fam, 40, 0xC0DE + FAMS.index(fam)):
+    _sweep(fam, _shapes(fam, 40, 0xC0DE + FAMS.index(fam)), random.Random(0x5EED + FAMS.index(fam)), 2)
+
+
+@pytest.mark.skipif(not os.environ.get("MEC_SWEEP_EXTENDED"), reason="one-off extended sweep (MEC_SWEEP_EXTENDED=<shapes>)")
+@pytest.mark.parametrize("fam", FAMS)
+def test_geometry_sweep_extended(fam):
+    """The same check over MEC_SWEEP_EXTENDED shapes per family with chunks
+    of 8 B-64 KiB (every launch shape the rules pick: one-wave / 4-wave
+    blocks, 8- / 16-byte bitmatrix lanes, the tiny in-place rule, tails),
+    another seed; run on demand, its log kept under profiles/."""
+    count = int(os.environ["MEC_SWEEP_EXTENDED"])
+    _sweep(fam, _shapes(fam, count, 0xE77 + FAMS.index(fam), max_units=8192), random.Random(0xE5 + FAMS.index(fam)), 3)
+
+
+def _sweep(fam, shapes, rng, n):
+    for (k, m, cs) in shapes:
         seed = rng.getrandbits(40)
         c = Codec(fam, k, m, cs)
         data = torch.empty(n * k * cs, dtype=torch.uint8, device=DEV)
