@@ -319,6 +319,16 @@ uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accum
     // RS(10,4)@1 MiB update 81.7 -> 84.1 %)
     if (accumulate && !in_place) return clampw(ceil_even(36.0 / std::max(1, rows)), 6, 20);
     const double w = 64.0 / std::max(1, k) + (in_place ? 2.0 : 1.0) * rows;
+    // split layouts: a dense matrix (decode into separate output chunks,
+    // ISA-L Cauchy encode) computes ~30 % longer per wave than the
+    // Vandermonde encode, so it wants more waves to keep as many reads in
+    // flight: ceil_even(64/K + 2R), at most 16, never below the split
+    // count (tools/split_cap_ab.py, tools/split_rule_ab.py,
+    // profiles/r03/gf8/split_*.log: RS(10,4)@1 MiB decode_split 80.3 ->
+    // 83.5 %, (12,4)@64 KiB 75.4 -> 83.1, (16,4)@256 KiB 70.5 -> 80.0,
+    // (20,4)@16 KiB 68.9 -> 80.6; 20 waves cost (4,2)@4 KiB 1.1-1.8)
+    if (!in_place && dense)
+        return std::max(clampw(ceil_even(w), 6, 20), std::min(ceil_even(64.0 / std::max(1, k) + 2.0 * rows), 16u));
     if (!in_place) return clampw(ceil_even(w), 6, 20);
     // a dense (decode) matrix keeps each wave busy longer than the
     // Vandermonde encode shortcut: at least 12 waves (RS(12,2) in-place
