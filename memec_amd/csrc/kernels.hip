@@ -327,9 +327,19 @@ uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accum
     // profiles/r03/gf8/split_*.log: RS(10,4)@1 MiB decode_split 80.3 ->
     // 83.5 %, (12,4)@64 KiB 75.4 -> 83.1, (16,4)@256 KiB 70.5 -> 80.0,
     // (20,4)@16 KiB 68.9 -> 80.6; 20 waves cost (4,2)@4 KiB 1.1-1.8)
+    // Wide stripes with 4 output rows want more waves than 64/K + R gives,
+    // since a wave's K x R products keep it computing longer: at least
+    // ceil_even(K/2 + 1), at most 16 (tools/enc_cap_ab.py,
+    // profiles/r03/gf8/enc_cap_ab.log, enc_rule_ab*.log: RS and ISA-L RS
+    // (16,4)@256 KiB encode +1.0-1.9 points, (20,4)@16 KiB +4.0, (24,4)@64
+    // KiB +5.1-5.8, (28,4)@4 KiB +4.1; k <= 12 unchanged).  Two rows lose
+    // 1-3 points with the same floor ((18,2), (22,2), (30,2)), so they keep
+    // the plain count.
+    const uint32_t floor_wide = rows >= 4 ? std::min(ceil_even(0.5 * k + 1.0), 16u) : 0u;
+    const uint32_t split = clampw(std::max(ceil_even(w), floor_wide), 6, 20);
     if (!in_place && dense)
-        return std::max(clampw(ceil_even(w), 6, 20), std::min(ceil_even(64.0 / std::max(1, k) + 2.0 * rows), 16u));
-    if (!in_place) return clampw(ceil_even(w), 6, 20);
+        return std::max(split, std::min(ceil_even(64.0 / std::max(1, k) + 2.0 * rows), 16u));
+    if (!in_place) return split;
     // a dense (decode) matrix keeps each wave busy longer than the
     // Vandermonde encode shortcut: at least 12 waves (RS(12,2) in-place
     // decode at 128-256 KiB chunks 71 -> 76 %, RS(14,2) +1-2 points;

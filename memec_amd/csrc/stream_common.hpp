@@ -219,7 +219,8 @@ uint32_t gathered_lds(uint32_t bt, uint32_t static_lds, uint8_t gshape);
 // (tools/wpc_ab.py, profiles/r02/wpc/).  The right count falls as a wave's
 // own in-flight reads grow and rises with its output streams:
 //   gf8 (all K source loads of a wave in flight at once)
-//     split outputs, Vandermonde:      ceil_even(64 / K + R),  6..20
+//     split outputs, Vandermonde:      ceil_even(64 / K + R), 6..20; with
+//                                      R = 4 at least min(ceil_even(K / 2 + 1), 16)
 //     split outputs, dense (decode_split, ISA-L Cauchy encode):
 //                          max(split count, min(ceil_even(64 / K + 2R), 16))
 //     read-modify-write (update):      ceil_even(36 / R),      6..20
