@@ -10,6 +10,12 @@ Run in the build container only (needs /root/reference and
   case metadata and SHA-256 digests at full BASELINE sizes;
 * ``golden.npz``   — raw expected output bytes for the small cases.
 
+The ISA-L family comes from oracle/_ref/libmemec_ref_isal.so: MemEC's own
+``common/coding`` compiled with -DUSE_ISAL over ISA-L 2.14's ec_base.c and
+ec_highlevel_func.c (oracle/ref_isal_plugin.cc has the recipe), so the
+plugin's glue — the survivor rows it inverts, the columns its
+startOff/endOff update touches — is the reference's own code.
+
 Inputs are never stored: they are regenerated from the splitmix64 stream
 (oracle.c ``orc_fill_splitmix`` == device ``mec_fill_random``) with the seed
 recorded per case.  Load the npz with ``allow_pickle=False``.
@@ -35,9 +41,22 @@ REF.ref_destroy.argtypes = [ctypes.c_void_p]
 REF.ref_encode.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint32, ctypes.c_uint32, u8p]
 REF.ref_decode.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint64]
 REF.ref_isal_gf_mul.restype = ctypes.c_uint8
-REF.ref_isal_plugin_decode.restype = ctypes.c_int
-REF.ref_isal_plugin_decode.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(u8p), ctypes.c_ulonglong]
-REF.ref_isal_plugin_encode.argtypes = [ctypes.c_int] * 4 + [ctypes.POINTER(u8p), u8p] + [ctypes.c_uint] * 3
+REFI = ctypes.CDLL(os.path.join(ROOT, "oracle", "_ref", "libmemec_ref_isal.so"))
+REFI.refi_instantiate.restype = ctypes.c_void_p
+REFI.refi_instantiate.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+REFI.refi_destroy.argtypes = [ctypes.c_void_p]
+REFI.refi_encode.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint32, u8p] + [ctypes.c_uint32] * 3
+REFI.refi_decode.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint64]
+REFI.refi_decode_poisoned.argtypes = [ctypes.c_void_p, u8p, ctypes.c_uint64, ctypes.c_uint8]
+ISAL_SCHEME = {"isal_rs": CS_RS, "isal_cauchy": CS_CAUCHY}
+
+
+def refi_encode(fam, k, m, cs, data, parity, index, st=0, ed=0, zero_mask=0):
+    """USE_ISAL Coding::encode(data, parity, index, startOff, endOff) on a
+    parity chunk holding `parity` (modified in place)."""
+    h = ctypes.c_void_p(REFI.refi_instantiate(ISAL_SCHEME[fam], k, m, cs))
+    REFI.refi_encode(h, ptr(data), zero_mask, ptr(parity), index, st, ed)
+    REFI.refi_destroy(h)
 
 
 def fill(n, seed, word_offset=0):
@@ -98,7 +117,7 @@ def ref_delta(scheme, k, m, cs, seed, col, index):
 
 def main():
     meta = {"generator": "tests/golden/make_golden.py",
-            "reference": "mtyiu/memec common/coding over lib/jerasure + lib/gf_complete; ISA-L 2.14 ec_base.c",
+            "reference": "mtyiu/memec common/coding over lib/jerasure + lib/gf_complete; the same plugin built USE_ISAL over ISA-L 2.14 ec_base.c + ec_highlevel_func.c",
             "prng": "splitmix64: word q = mix(seed + (q+1)*0x9E3779B97F4A7C15), little-endian bytes",
             "cases": {}}
     blobs = {}
@@ -239,9 +258,17 @@ def main():
             data = fill(k * cs, s)
             par = np.zeros(m * cs, dtype=np.uint8)
             coef = a[k * k:].copy()
+            # the plugin's encode, one call per parity index (coding.cc:150-152)
+            for i in range(m):
+                one = np.zeros(cs, dtype=np.uint8)
+                refi_encode(fam, k, m, cs, data, one, i + 1)
+                par[i * cs:(i + 1) * cs] = one
+            # == ISA-L's own ec_encode_data_base over gf_vect_mul_init tables
+            chk = np.zeros(m * cs, dtype=np.uint8)
             src = (u8p * k)(*[ptr(data[j * cs:]) for j in range(k)])
-            dst = (u8p * m)(*[ptr(par[i * cs:]) for i in range(m)])
+            dst = (u8p * m)(*[ptr(chk[i * cs:]) for i in range(m)])
             REF.ref_isal_encode(cs, k, m, ptr(coef), src, dst)
+            assert np.array_equal(par, chk), (fam, k, m)
             name = "enc/%s/%d_%d_%d_x1" % (fam, k, m, cs)
             blobs[name] = par
             meta["cases"][name] = {"kind": "encode", "family": fam, "k": k, "m": m, "chunk": cs, "stripes": 1,
@@ -260,14 +287,15 @@ def main():
     meta["isal_matrices"] = isal
 
     # --- ISA-L plugin decode (USE_ISAL RSCoding/CauchyCoding::decode) ----------------
-    # Random non-codeword stripes through the plugin's own steps
-    # (rscoding.cc:155-177, cauchycoding.cc:145-168; oracle/ref_isal_shim.c
-    # ref_isal_plugin_decode).  Erased DATA chunks are the reference's
-    # output.  For an erased PARITY chunk the plugin reads past the k x k
-    # inverse (uninitialised bytes; zero in the shim), so the fixture also
-    # holds `fixed`: the reference's own ISA-L encode (ref_isal_plugin_encode)
-    # of the data after the reference's decode — the value a correct decode
-    # writes there.
+    # Random non-codeword stripes through the reference plugin itself
+    # (rscoding.cc:97-187, cauchycoding.cc:87-180, libmemec_ref_isal.so).
+    # Erased DATA chunks are the reference's output bit for bit.  For an
+    # erased PARITY chunk the plugin reads rows past the k x k inverse, i.e.
+    # uninitialised stack (rscoding.cc:173-175): its bytes are undefined, so
+    # the blob holds zeros there, `fixed` holds the reference plugin's own
+    # encode of the decoded data (what a correct decode writes),
+    # and `reference_parity_defect` records that the plugin's output, with
+    # the stack poisoned, differs from `fixed` in every such chunk.
     isal_dec = [
         (4, 2, [[0], [1, 3], [0, 1], [4], [5], [4, 5], [0, 4], [3, 5]]),
         (10, 4, [[0, 1, 2, 3], [0, 5, 9], [3], [9], [10], [13], [10, 11, 12, 13], [0, 5, 10, 13], [2, 7, 11],
@@ -282,36 +310,50 @@ def main():
                 s = seed + 5000 + 1000 * fam_i + 100 * idx + p_i
                 chunks = fill((k + m) * cs, s)
                 present = sum(1 << i for i in range(k + m) if i not in pat)
-                work = chunks.copy()
-                for e in pat:
-                    work[e * cs:(e + 1) * cs] = 0
-                cp = (u8p * (k + m))(*[ptr(work[i * cs:]) for i in range(k + m)])
-                rc = REF.ref_isal_plugin_decode(fam_i, k, m, cs, cp, present)
+                outs = []
+                for poison in (0x00, 0xA5):
+                    work = chunks.copy()
+                    for e in pat:
+                        work[e * cs:(e + 1) * cs] = 0
+                    h = ctypes.c_void_p(REFI.refi_instantiate(ISAL_SCHEME[fam], k, m, cs))
+                    rc = REFI.refi_decode_poisoned(h, ptr(work), ctypes.c_uint64(present), poison)
+                    REFI.refi_destroy(h)
+                    outs.append(work)
+                work = outs[1]
                 out = np.concatenate([work[e * cs:(e + 1) * cs] for e in sorted(pat)])
+                # erased data chunks do not depend on the stack
+                for e in pat:
+                    if e < k:
+                        assert np.array_equal(outs[0][e * cs:(e + 1) * cs], work[e * cs:(e + 1) * cs]), (fam, pat)
                 # reference re-encode of the decoded data -> correct parity
                 fixed = out.copy()
+                defect = []
                 for r, e in enumerate(sorted(pat)):
                     if e < k:
                         continue
-                    dp = (u8p * k)(*[ptr(work[j * cs:]) for j in range(k)])
                     par = np.zeros(cs, np.uint8)
-                    REF.ref_isal_plugin_encode(fam_i, k, m, cs, dp, ptr(par), e - k + 1, 0, 0)
+                    refi_encode(fam, k, m, cs, work[:k * cs].copy(), par, e - k + 1)
                     fixed[r * cs:(r + 1) * cs] = par
+                    defect.append(bool(not np.array_equal(out[r * cs:(r + 1) * cs], par)))
+                    out[r * cs:(r + 1) * cs] = 0
                 name = "dec/%s/%d_%d_%d/%s" % (fam, k, m, cs, "-".join(map(str, pat)))
                 blobs[name] = out
                 blobs[name + "|fixed"] = fixed
                 meta["cases"][name] = {"kind": "decode_random_isal", "family": fam, "k": k, "m": m, "chunk": cs,
-                                       "seed": s, "erased": pat, "rc": rc,
+                                       "seed": s, "erased": pat, "rc": 1 if rc == 0 else 0,
+                                       "reference_parity_defect": defect,
                                        "input_layout": "[k+m][chunk] random; erased chunks cleared before decode",
-                                       "output_layout": "erased chunks ascending (reference plugin output)",
-                                       "fixed_layout": "same; erased parity replaced by the reference's ISA-L "
-                                                       "encode of the decoded data"}
+                                       "output_layout": "erased chunks ascending (reference plugin output; "
+                                                        "erased parity undefined there, zeroed)",
+                                       "fixed_layout": "same; erased parity = the reference plugin's encode "
+                                                       "of the decoded data"}
 
     # --- ISA-L plugin encode with startOff/endOff (the server's delta call) -------------
     # RSCoding::encode's USE_ISAL update branch XORs ec_encode_data_update
     # over data columns [startOff/chunk, (endOff-1)/chunk] into the caller's
     # parity (rscoding.cc:82-89); CauchyCoding ignores the offsets and
-    # overwrites it with a full ec_encode_data (cauchycoding.cc:78-79).
+    # overwrites it with a full ec_encode_data (cauchycoding.cc:78-79).  Both
+    # run as the reference plugin's own encode here.
     for fam_i, fam in enumerate(("isal_rs", "isal_cauchy")):
         for idx, (k, m, cs, index, st, ed) in enumerate([(10, 4, 512, 2, 3 * 512 + 100, 5 * 512 + 7),
                                                         (4, 2, 4096, 1, 0, 4096), (6, 3, 256, 3, 1 * 256, 2 * 256),
@@ -319,15 +361,15 @@ def main():
             s = seed + 7000 + 100 * fam_i + idx
             data = fill(k * cs, s)
             par = fill(cs, s + 1)
-            dp = (u8p * k)(*[ptr(data[j * cs:]) for j in range(k)])
-            REF.ref_isal_plugin_encode(fam_i, k, m, cs, dp, ptr(par), index, st, ed)
+            refi_encode(fam, k, m, cs, data, par, index, st, ed)
             name = "encoff/%s/%d_%d_%d/i%d_s%d_e%d" % (fam, k, m, cs, index, st, ed)
             blobs[name] = par
             meta["cases"][name] = {"kind": "encode_offsets_isal", "family": fam, "k": k, "m": m, "chunk": cs,
                                    "seed": s, "parity_seed": s + 1, "index": index, "startOff": st, "endOff": ed,
                                    "data_layout": "[k][chunk] splitmix(seed)",
                                    "parity_in": "[chunk] splitmix(parity_seed), the caller's parity chunk",
-                                   "expected": "the caller's parity chunk after RSCoding/CauchyCoding::encode"}
+                                   "expected": "the caller's parity chunk after the reference plugin's "
+                                               "RSCoding/CauchyCoding::encode (USE_ISAL)"}
 
     np.savez_compressed(os.path.join(HERE, "golden.npz"), **{k.replace("/", "|"): v for k, v in blobs.items()})
     with open(os.path.join(HERE, "golden.json"), "w") as f:

@@ -158,12 +158,12 @@ def test_decode_matches_reference_fixtures(golden):
 
 
 def test_isal_decode_matches_reference_plugin(golden):
-    """USE_ISAL decode vs the reference plugin's own steps
-    (rscoding.cc:155-177, cauchycoding.cc:145-168 over ISA-L ec_base.c):
-    erased data chunks equal the reference's output; erased parity chunks
-    equal the reference's ISA-L encode of the decoded data (`fixed`) and
-    differ from the reference's output, which reads past the k x k inverse
-    (DESIGN §8)."""
+    """USE_ISAL decode vs the reference plugin itself (rscoding.cc /
+    cauchycoding.cc built -DUSE_ISAL over ISA-L ec_base.c,
+    oracle/ref_isal_plugin.cc): erased data chunks equal the reference's
+    output; erased parity chunks equal the reference plugin's encode of the
+    decoded data (`fixed`) — the reference's own output there reads past the
+    k x k inverse into uninitialised stack."""
     meta, blobs = golden
     cases = [(n, c) for n, c in sorted(meta["cases"].items()) if c["kind"] == "decode_random_isal"]
     assert len(cases) >= 60
@@ -178,7 +178,8 @@ def test_isal_decode_matches_reference_plugin(golden):
         ref, fixed = blobs[name], blobs[name + "/fixed"]
         for r, e in enumerate(sorted(c["erased"])):
             assert np.array_equal(got[e], fixed[r * cs:(r + 1) * cs]), (name, e)
-            assert np.array_equal(got[e], ref[r * cs:(r + 1) * cs]) == (e < k), (name, e)
+            if e < k:
+                assert np.array_equal(got[e], ref[r * cs:(r + 1) * cs]), (name, e)
         orig = O.fill((k + m) * cs, c["seed"]).reshape(k + m, cs)
         for i in range(k + m):
             if i not in c["erased"]:
