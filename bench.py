@@ -799,6 +799,15 @@ def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_
     return res
 
 
+def runs_cpu_legs(rank, world, disabled):
+    """Whether this rank times the reference CPU path (cpu_baseline, the
+    decode twin's baseline, configs[0]'s reference_cpu): rank 0 at every N —
+    the 2/4/8-GPU lines carry the baseline as the 1-GPU line does — after
+    every rank's GPU legs (main's barrier), never inside a timed region."""
+    del world  # every world size
+    return rank == 0 and not disabled
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -928,7 +937,7 @@ def main():
         present = sum(1 << i for i in range(k + m) if i not in erased)
         orig = stripe[:, erased].clone() if stripes * len(erased) * cs <= (24 << 30) else None
         codewords_np = None  # CPU-baseline sample: GPU-encoded stripes before the erasure
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if runs_cpu_legs(rank, world, args.no_cpu_baseline):
             threads_cb = args.cpu_threads or host_cores()[0]
             codewords_np = stripe[:cpu_sample(k, m, cs, threads_cb)].cpu().numpy()
         # random non-codewords planted in the second half pin the survivor
@@ -955,7 +964,7 @@ def main():
     parity_pin, ok, gpu_parity_np = None, None, None
     if op == "encode":
         parity_pin = pin(check_encode(fam, k, m, cs, data, parity))
-        if rank == 0 and not args.no_cpu_baseline:
+        if runs_cpu_legs(rank, world, args.no_cpu_baseline):
             gpu_parity_np = parity[:64].cpu().numpy()
     elif op == "decode":
         parity_pin = pin(check_decode(fam, k, m, cs, stripe, erased, nc_rec))
@@ -997,7 +1006,7 @@ def main():
         st[:, :k] = data
         st[:, k:] = parity
         dcodewords = None  # CPU-baseline sample of the twin: GPU-encoded codewords
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if runs_cpu_legs(rank, world, args.no_cpu_baseline):
             dcodewords = st[:cpu_sample(k, m, cs, args.cpu_threads or host_cores()[0])].cpu().numpy()
         saved = st[:, derased].clone()
         drec = plant_noncodewords(st, k, m, cs, 0x5EED + 7 * rank + 1)
@@ -1086,6 +1095,14 @@ def main():
                          "registered": "mec_host_register: kernel reads/writes host memory over PCIe (zero-copy)"},
                **res}
 
+    # every rank's GPU work (timed legs, pins, verifications) ends here; the
+    # CPU legs below run on rank 0 alone, outside every timed region, while
+    # the other ranks leave (a rank parked in an RCCL barrier would spin a
+    # host core the reference's threads need), as the reference runs its
+    # batch benchmark as worker threads on one host
+    # (test/common/coding/batch_performance.cc:143-154)
+    if use_pg:
+        dist.barrier()
     if rank == 0:
         traffic, traffic_src = load_traffic(args.config, stripes)
         # data GiB/s: k data chunks per stripe (encode / decode), the one
@@ -1137,7 +1154,7 @@ def main():
             line["e2e_host_memory"] = e2e
         if extras:
             line["other_configs"] = extras
-            if "configs[0]" in extras and world == 1 and not args.no_cpu_baseline:
+            if "configs[0]" in extras and runs_cpu_legs(rank, world, args.no_cpu_baseline):
                 # configs[0] is the reference's own CPU path: time it here too
                 try:
                     extras["configs[0]"]["reference_cpu"] = configs0_reference()
@@ -1145,7 +1162,7 @@ def main():
                     extras["configs[0]"]["reference_cpu"] = {"error": repr(exc)}
         if secondary:
             line["decode"] = secondary
-        if not args.no_cpu_baseline and world == 1:
+        if runs_cpu_legs(rank, world, args.no_cpu_baseline):
             threads, host = host_cores()
             threads = args.cpu_threads or threads
             try:
@@ -1175,6 +1192,8 @@ def main():
             for cb in (line["cpu_baseline"], (secondary or {}).get("cpu_baseline")):
                 if cb and "error" not in cb:
                     cb["host"] = dict(host, threads_used=threads)
+                    cb["when"] = ("rank 0 of %d, after every rank finished its GPU legs (barrier), other ranks "
+                                  "exited; sample from rank 0's stripes" % world)
         print(json.dumps(line), flush=True)
     if use_pg:
         dist.destroy_process_group()

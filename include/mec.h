@@ -304,10 +304,14 @@ int mec_set_coalescing(mec_ctx *ctx, uint32_t max_batch);
  * Timeout: a call not completed within MEC_QUEUE_TIMEOUT_MS (default 5000)
  * withdraws its job, stops the queue FOR GOOD (mec_stats.queue_broken = 1,
  * queue_timeouts counts them; every later call takes the launch path until
- * mec_set_host_queue is called again) and waits — without a time limit —
- * until the resident kernel has left, so no queue work can still write the
- * caller's chunks when the call returns; a job that never ran is then coded
- * on the launch path.
+ * mec_set_host_queue is called again) and waits for the resident kernel to
+ * leave, at most max(4 x MEC_QUEUE_TIMEOUT_MS, 10 s).  Then: a job every part of its
+ * slot finished returns MEC_OK; a job no part took is coded on the launch
+ * path; anything else — some parts finished, the kernel faulted, or it is
+ * still running at the cap — returns MEC_EHIP and the outputs are undefined
+ * (a still-running kernel may write them later; the slot stays reserved and
+ * mec_destroy leaks the queue's memory rather than free it under the
+ * kernel).
  * 0 stops the queue.  Not to be called concurrently with other calls on the
  * context.  Replaces nothing in the reference: its workers call the CPU
  * plugin directly (worker.cc:128-137). */
@@ -332,8 +336,10 @@ int mec_set_probe(mec_ctx *ctx, int mode);
  * MEC_BLOCK, MEC_GBLOCK, MEC_GWPC, MEC_BM_VW, MEC_WPC and MEC_COPY_THREADS
  * from the environment once, at first use, never on a launch path; this
  * call changes one at run time (same name and value syntax as the
- * variable; value NULL = unset, i.e. the built-in rule).  Changes are
- * atomic: a launch running concurrently sees the old or the new value.
+ * variable; value NULL = unset, i.e. the built-in rule).  Each stored
+ * value is one atomic word, so a concurrent launch sees the old or the new
+ * value of it; MEC_SGROUP's group and run are two words, and a launch racing
+ * a change may see one of each (experiments set knobs between launches).
  * MEC_EINVAL for an unknown name. */
 int mec_set_knob(const char *name, const char *value);
 

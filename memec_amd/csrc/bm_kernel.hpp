@@ -205,7 +205,7 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
             if (L.stab) {
                 p.s0 = s0;
-                if constexpr (VW == bm_vw<W>()) {
+                if constexpr (VW == bm_vw<W>() && R <= kMaxRows) {
                     const uint32_t glds = gathered_lds(bt, 0, gshape);
                     if (bt == kWaveBlock)
                         hipLaunchKernelGGL((bm_kernel<W, R, true, kWaveBlock>), dim3(ns * g.tiles), dim3(bt), glds, stream, p);
@@ -222,10 +222,6 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
                 p.nstr = ns;
                 p.sgroup = stripe_group(p.chunk, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, true, p.srun);
                 const bool in_place = p.win > 1;
-                if (p.sgroup == kStripePerm) {  // the permutation replaces the windows
-                    p.win = 1;
-                    p.sgroup = stripe_group(p.chunk, g.tiles, ns, in_place, true, p.srun);
-                }
                 const uint32_t lds = occupancy_lds(bt, std::min<uint32_t>(bt, g.units), 0, bm_target_waves(R, W, VW, in_place));
                 if (bt == kWaveBlock)
                     hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock, VW>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
@@ -255,11 +251,13 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     return run_bm_vw<W, R, bm_vw<W>()>(L, stream);
 }
 
-#define MEC_BM_INSTANTIATE_W(W) \
-    template hipError_t run_bm<W, 1>(const BmLaunch &, hipStream_t); \
-    template hipError_t run_bm<W, 2>(const BmLaunch &, hipStream_t); \
-    template hipError_t run_bm<W, 3>(const BmLaunch &, hipStream_t); \
-    template hipError_t run_bm<W, 4>(const BmLaunch &, hipStream_t);
+#define MEC_BM_ONE(W, R) template hipError_t run_bm<W, R>(const BmLaunch &, hipStream_t);
+#define MEC_BM_EXT(W, R) extern template hipError_t run_bm<W, R>(const BmLaunch &, hipStream_t);
+#define MEC_FOR_R4(X, W) X(W, 1) X(W, 2) X(W, 3) X(W, 4)
+#define MEC_FOR_R8(X, W) MEC_FOR_R4(X, W) X(W, 5) X(W, 6) X(W, 7) X(W, 8)
+#define MEC_FOR_W(F, X) F(X, 1) F(X, 2) F(X, 3) F(X, 4) F(X, 5) F(X, 6) F(X, 7) F(X, 8)
+// strided launches take up to kMaxBmOut outputs (R = 1..8), gathered ones 4
+#define MEC_BM_INSTANTIATE_W(W) MEC_FOR_R8(MEC_BM_ONE, W)
 
 }  // namespace detail
 }  // namespace mec

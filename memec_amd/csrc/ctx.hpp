@@ -108,6 +108,9 @@ struct Coalescer {
 // queue.hip: device-side submission queue for single-stripe host calls.
 constexpr uint32_t kQMaxSrc = 32, kQMaxDst = 4, kQMaxSlots = 1024;
 constexpr uint32_t kQMaxParts = 64;  // workgroups per slot (one call's chunk spread over CUs)
+// a timed-out call waits at most this many call timeouts (at least 10 s)
+// for the resident grid to leave before it gives up with MEC_EHIP (queue_try)
+constexpr uint64_t kQDrainFactor = 4;
 constexpr uint32_t kQBmRows = kQMaxDst * 8;  // bitmatrix output packet rows (outputs x w <= 8)
 struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
     uint64_t seq;            // host -> GPU: number of the posted job
@@ -177,6 +180,10 @@ struct mec_ctx {
     // mec_set_probe: MEC_PROBE_XOR runs strided byte-wise launches as their
     // arithmetic-free twin (measurement only)
     std::atomic<int> probe{0};
+    // device copies of the permute tables of > 4-row matrices
+    // (gf8_mg_kernel), keyed by (rows, k, coefficient bytes); uploaded once
+    std::mutex mg_mu;
+    std::unordered_map<std::string, uint32_t *> mg_tabs;
 
     bool byte_wise() const { return family != MEC_CAUCHY_GOOD; }
     mec::Scheme scheme() const {

@@ -221,20 +221,12 @@ hipError_t run_bm_gather(const GatherLaunch &L, hipStream_t stream) {
 }
 
 #define MEC_GG8_ONE(K, R) template hipError_t run_gf8_gather<K, R>(const GatherLaunch &, hipStream_t);
-#define MEC_GG8_INSTANTIATE_LO(R)                                                                              \
-    MEC_GG8_ONE(1, R) MEC_GG8_ONE(2, R) MEC_GG8_ONE(3, R) MEC_GG8_ONE(4, R) MEC_GG8_ONE(5, R) MEC_GG8_ONE(6, R) \
-    MEC_GG8_ONE(7, R) MEC_GG8_ONE(8, R) MEC_GG8_ONE(9, R) MEC_GG8_ONE(10, R) MEC_GG8_ONE(11, R)                \
-    MEC_GG8_ONE(12, R) MEC_GG8_ONE(13, R) MEC_GG8_ONE(14, R) MEC_GG8_ONE(15, R) MEC_GG8_ONE(16, R)
-#define MEC_GG8_INSTANTIATE_HI(R)                                                                          \
-    MEC_GG8_ONE(17, R) MEC_GG8_ONE(18, R) MEC_GG8_ONE(19, R) MEC_GG8_ONE(20, R) MEC_GG8_ONE(21, R)        \
-    MEC_GG8_ONE(22, R) MEC_GG8_ONE(23, R) MEC_GG8_ONE(24, R) MEC_GG8_ONE(25, R) MEC_GG8_ONE(26, R)        \
-    MEC_GG8_ONE(27, R) MEC_GG8_ONE(28, R) MEC_GG8_ONE(29, R) MEC_GG8_ONE(30, R) MEC_GG8_ONE(31, R)        \
-    MEC_GG8_ONE(32, R)
-#define MEC_GBM_INSTANTIATE_W(W)                                                   \
-    template hipError_t run_bm_gather<W, 1>(const GatherLaunch &, hipStream_t); \
-    template hipError_t run_bm_gather<W, 2>(const GatherLaunch &, hipStream_t); \
-    template hipError_t run_bm_gather<W, 3>(const GatherLaunch &, hipStream_t); \
-    template hipError_t run_bm_gather<W, 4>(const GatherLaunch &, hipStream_t);
+#define MEC_GG8_EXT(K, R) extern template hipError_t run_gf8_gather<K, R>(const GatherLaunch &, hipStream_t);
+#define MEC_GG8_INSTANTIATE_LO(R) MEC_FOR_K_LO(MEC_GG8_ONE, R)
+#define MEC_GG8_INSTANTIATE_HI(R) MEC_FOR_K_HI(MEC_GG8_ONE, R)
+#define MEC_GBM_ONE(W, R) template hipError_t run_bm_gather<W, R>(const GatherLaunch &, hipStream_t);
+#define MEC_GBM_EXT(W, R) extern template hipError_t run_bm_gather<W, R>(const GatherLaunch &, hipStream_t);
+#define MEC_GBM_INSTANTIATE_W(W) MEC_FOR_R4(MEC_GBM_ONE, W)
 
 }  // namespace detail
 }  // namespace mec

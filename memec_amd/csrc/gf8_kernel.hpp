@@ -16,6 +16,8 @@
 // live in LDS (R*K*32 bytes) and are read by broadcast right before use.
 #pragma once
 
+#include <vector>
+
 #include "stream_common.hpp"
 
 namespace mec {
@@ -69,9 +71,12 @@ __device__ __forceinline__ u32x4 xor3(const u32x4 &a, const u32x4 &b, const u32x
 //   kGf8Xor   — measurement twin (mec_set_probe): every product replaced by
 //               a plain XOR, same loads, stores and launch shape; the
 //               outputs are not codes.
+//   kGf8Col0  — column 0 all ones only: the row groups after the first of a
+//               Vandermonde matrix with more than one group (gf8_mg_kernel).
 constexpr int kGf8Dense = 0;
 constexpr int kGf8Vand = 1;
 constexpr int kGf8Xor = 2;
+constexpr int kGf8Col0 = 3;
 
 // acc[i] ^= sum_j coef(i, j) * d[j] for one 16-byte unit.  TB = the LDS
 // permute tables (8 dwords per coefficient b = i*K + j: t0 t1 u0 u1 v).
@@ -107,7 +112,7 @@ __device__ __forceinline__ void gf8_apply(const u32x4 (&d)[K], u32x4 (&acc)[R], 
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         const u32x4 x = d[j];
-        if (S == kGf8Vand && j == 0) {
+        if ((S == kGf8Vand || S == kGf8Col0) && j == 0) {
 #pragma unroll
             for (int i = 0; i < R; ++i) put(i, x);
             continue;
@@ -199,6 +204,78 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
 }
 
+// More than 4 outputs (m > 4: RS(16,8), ISA-L RS(12,8), decodes of > 4
+// erasures) in ONE pass over the sources: a lane loads its K source units
+// once and codes `groups` row groups of R outputs from the same registers,
+// one group at a time (the register footprint of an R-row launch), so the
+// sources are read once however many outputs there are — the 4-row launches
+// before re-read them ceil(m / 4) times (RS(16,8): 1.67x the algorithmic
+// bytes).  The groups' permute tables (groups x R x K x 8 dwords, row r of
+// group g at (g * R + r) * K * 8) come from a device copy (gf8_mg_tables)
+// into dynamic LDS; rows past the last output are padding (dst_off < 0: no
+// store).  S = kGf8Vand: group 0 has row 0 and column 0 all ones, the others
+// column 0 (Jerasure / ISA-L RS parity rows); kGf8Dense otherwise.  One-wave
+// blocks, strided layouts only (pointer batches split rows in groups of 4).
+template <int K>
+struct Gf8MgParams {
+    const uint8_t *src;
+    uint8_t *dst;
+    int64_t sss, dss;
+    const uint32_t *tabs;  // device: groups x R x K x 8 dwords
+    uint32_t chunk, units, tiles, accumulate, win, nstr, sgroup, srun, groups, pad;
+    int64_t src_off[K];
+    int64_t dst_off[kMaxSrc];  // groups x R rows; < 0 = padding
+};
+
+template <int K, int R, int S>
+__global__ __launch_bounds__(kWaveBlock) void gf8_mg_kernel(const Gf8MgParams<K> p) {
+    extern __shared__ uint32_t mtab[];
+    const uint32_t ntab = p.groups * R * K * 8;
+    for (uint32_t t = threadIdx.x; t < ntab; t += kWaveBlock) mtab[t] = p.tabs[t];
+    __syncthreads();
+    const uint32_t bid = block_order(p.win);
+    uint32_t stripe, tile;
+    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, stripe, tile);
+    const uint32_t u = tile * kWaveBlock + threadIdx.x;
+    if (u >= p.units) return;
+    const uint32_t off = u * 16;
+    u32x4 d[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j)
+        d[j] = buf_ld<u32x4>(chunk_rsrc(uint64_t(uintptr_t(p.src + int64_t(stripe) * p.sss + p.src_off[j])), p.chunk),
+                             off, true);
+    uint8_t *db = p.dst + int64_t(stripe) * p.dss;
+    auto group = [&](uint32_t g, auto apply) {
+        __amdgpu_buffer_rsrc_t dr[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int64_t o = p.dst_off[g * R + i];
+            dr[i] = chunk_rsrc(o < 0 ? 0 : uint64_t(uintptr_t(db + o)), p.chunk);
+        }
+        u32x4 acc[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
+        apply(acc, mtab + g * (R * K * 8) + opaque_zero());
+#pragma unroll
+        for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
+    };
+    // group 0 (row 0 all ones for kGf8Vand), then the rest; the sources
+    // "change" before every group (an empty asm), so the compiler cannot
+    // hoist their bit fields out of the loop (3 x K x 4 more live VGPRs:
+    // K = 17 ran at 256 VGPRs, occupancy 1)
+    group(0, [&](u32x4 (&acc)[R], const uint32_t *tb) { gf8_apply<K, R, S>(d, acc, tb); });
+    for (uint32_t g = 1; g < p.groups; ++g) {  // uniform
+#pragma unroll
+        for (int j = 0; j < K; ++j) asm volatile("" : "+v"(d[j]));
+        group(g, [&](u32x4 (&acc)[R], const uint32_t *tb) {
+            gf8_apply<K, R, S == kGf8Vand ? kGf8Col0 : kGf8Dense>(d, acc, tb);
+        });
+    }
+}
+
+template <int K, int R>
+hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream);
+
 // The < 16-byte remainder of each region (chunk sizes that are not a
 // multiple of 16): one thread per stripe, any K and row count.
 struct Gf8TailParams {
@@ -278,10 +355,6 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                 p.nstr = ns;
                 p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
                 const bool in_place = p.win > 1;
-                if (p.sgroup == kStripePerm) {  // the permutation replaces the windows
-                    p.win = 1;
-                    p.sgroup = stripe_group(L.len, g.tiles, ns, in_place, false, p.srun);
-                }
                 const dim3 grid(ns * g.tiles), block(bt);
                 const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, in_place, !vand, L.accumulate));
                 if (L.probe) {
@@ -309,14 +382,50 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     return hipSuccess;
 }
 
+template <int K, int R>
+hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
+    Gf8MgParams<K> p;
+    p.sss = L.src_stripe_stride;
+    p.dss = L.dst_stripe_stride;
+    p.tabs = L.tabs;
+    p.chunk = uint32_t(L.len);
+    const Geometry g = geometry(L.len / 16, kWaveBlock);
+    p.units = g.units;
+    p.tiles = g.tiles;
+    p.accumulate = L.accumulate ? 1u : 0u;
+    p.groups = uint32_t((L.rows + R - 1) / R);
+    p.pad = 0;
+    for (int j = 0; j < K; ++j) p.src_off[j] = L.src_off[j];
+    for (int r = 0; r < kMaxSrc; ++r) p.dst_off[r] = r < L.rows ? L.dst_off[r] : -1;
+    const uint32_t tab_bytes = p.groups * R * K * 32;
+    if (g.units == 0) return hipSuccess;
+    for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
+        const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
+        p.src = L.src + int64_t(s0) * L.src_stripe_stride;
+        p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+        p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
+        p.nstr = ns;
+        p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
+        // the tables are the block's LDS; the wave cap may reserve more
+        const uint32_t cap = occupancy_lds(kWaveBlock, kWaveBlock, 0,
+                                           gf8_target_waves(K, L.rows, p.win > 1, !L.vand, L.accumulate));
+        const uint32_t lds = std::max(cap, tab_bytes);
+        if (L.vand)
+            hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Vand>), dim3(ns * g.tiles), dim3(kWaveBlock), lds, stream, p);
+        else
+            hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Dense>), dim3(ns * g.tiles), dim3(kWaveBlock), lds, stream, p);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 #define MEC_GF8_ONE(K, R) template hipError_t run_gf8<K, R>(const Gf8Launch &, hipStream_t);
-// K = 1..16 and 17..32 in separate translation units (parallel builds).
-#define MEC_GF8_INSTANTIATE_LO(R) \
-    MEC_GF8_ONE(1, R) MEC_GF8_ONE(2, R) MEC_GF8_ONE(3, R) MEC_GF8_ONE(4, R) MEC_GF8_ONE(5, R) MEC_GF8_ONE(6, R) MEC_GF8_ONE(7, R) MEC_GF8_ONE(8, R) \
-    MEC_GF8_ONE(9, R) MEC_GF8_ONE(10, R) MEC_GF8_ONE(11, R) MEC_GF8_ONE(12, R) MEC_GF8_ONE(13, R) MEC_GF8_ONE(14, R) MEC_GF8_ONE(15, R) MEC_GF8_ONE(16, R)
-#define MEC_GF8_INSTANTIATE_HI(R) \
-    MEC_GF8_ONE(17, R) MEC_GF8_ONE(18, R) MEC_GF8_ONE(19, R) MEC_GF8_ONE(20, R) MEC_GF8_ONE(21, R) MEC_GF8_ONE(22, R) MEC_GF8_ONE(23, R) MEC_GF8_ONE(24, R) \
-    MEC_GF8_ONE(25, R) MEC_GF8_ONE(26, R) MEC_GF8_ONE(27, R) MEC_GF8_ONE(28, R) MEC_GF8_ONE(29, R) MEC_GF8_ONE(30, R) MEC_GF8_ONE(31, R) MEC_GF8_ONE(32, R)
+#define MEC_GF8_EXT(K, R) extern template hipError_t run_gf8<K, R>(const Gf8Launch &, hipStream_t);
+#define MEC_GF8_INSTANTIATE_LO(R) MEC_FOR_K_LO(MEC_GF8_ONE, R)
+#define MEC_GF8_INSTANTIATE_HI(R) MEC_FOR_K_HI(MEC_GF8_ONE, R)
+#define MEC_GFM_ONE(K, R) template hipError_t run_gf8_mg<K, R>(const Gf8MgLaunch &, hipStream_t);
+#define MEC_GFM_EXT(K, R) extern template hipError_t run_gf8_mg<K, R>(const Gf8MgLaunch &, hipStream_t);
 
 }  // namespace detail
 }  // namespace mec

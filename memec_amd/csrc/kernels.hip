@@ -42,6 +42,12 @@ template <int K, int R>
 hipError_t run_gf8_gather(const GatherLaunch &L, hipStream_t stream);
 template <int W, int R>
 hipError_t run_bm_gather(const GatherLaunch &L, hipStream_t stream);
+// instantiated in gf8_r*.hip, gg8_r*.hip, bm_w*.hip and gbm.hip, never here
+MEC_FOR_K(MEC_GF8_EXT, 1) MEC_FOR_K(MEC_GF8_EXT, 2) MEC_FOR_K(MEC_GF8_EXT, 3) MEC_FOR_K(MEC_GF8_EXT, 4)
+MEC_FOR_K(MEC_GFM_EXT, 3) MEC_FOR_K(MEC_GFM_EXT, 4)
+MEC_FOR_K(MEC_GG8_EXT, 1) MEC_FOR_K(MEC_GG8_EXT, 2) MEC_FOR_K(MEC_GG8_EXT, 3) MEC_FOR_K(MEC_GG8_EXT, 4)
+MEC_FOR_W(MEC_FOR_R8, MEC_BM_EXT)
+MEC_FOR_W(MEC_FOR_R4, MEC_GBM_EXT)
 
 // Gathered tails: the < unit remainder of each region, one thread per
 // stripe, any k / rows / w, reading the descriptor blob directly.
@@ -160,7 +166,7 @@ struct BmTailParams {
     uint64_t packet, off;
     uint32_t n, k, rows, w, n_stripes, accumulate;
     int64_t src_off[kMaxSrc];
-    int64_t dst_off[kMaxRows];
+    int64_t dst_off[kMaxBmOut];
     uint8_t mask[kMaxSrc][kMaxBmRows];
 };
 
@@ -207,7 +213,7 @@ hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream) {
     p.n_stripes = L.n_stripes;
     p.accumulate = L.accumulate ? 1u : 0u;
     for (int j = 0; j < kMaxSrc; ++j) p.src_off[j] = L.src_off[j];
-    for (int i = 0; i < kMaxRows; ++i) p.dst_off[i] = L.dst_off[i];
+    for (int i = 0; i < kMaxBmOut; ++i) p.dst_off[i] = L.dst_off[i];
     for (int j = 0; j < kMaxSrc; ++j)
         for (int r = 0; r < kMaxBmRows; ++r) p.mask[j][r] = L.mask[j][r];
     hipLaunchKernelGGL(bm_tail_kernel, dim3((L.n_stripes + kThreads - 1) / kThreads), dim3(kThreads), 0, stream, p);
@@ -234,22 +240,6 @@ uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool i
     (void)in_place;
     uint32_t g = (!bitmatrix && chunk >= (uint64_t(2) << 20)) ? 16u : 0u;
     if (kg != kKnobUnset) {
-        if (kg == kKnobXcd) return tiles % 8 == 0 ? kXcdRegions : 0u;
-        if (kg == kKnobPerm) {  // a multiplier coprime to n_stripes near n / golden ratio
-            if (n_stripes < 2) return 0;
-            uint64_t mlt = kr != kKnobUnset && kr > 0 ? uint64_t(kr) : uint64_t(double(n_stripes) * 0.6180339887) | 1u;
-            auto gcd = [](uint64_t a, uint64_t b) {
-                while (b) {
-                    const uint64_t t = a % b;
-                    a = b;
-                    b = t;
-                }
-                return a;
-            };
-            while (gcd(mlt % n_stripes, n_stripes) != 1) mlt += 1;
-            run = uint32_t(mlt % n_stripes);
-            return kStripePerm;
-        }
         g = uint32_t(std::max<int64_t>(kg, 0));
         if (kr != kKnobUnset) run = uint32_t(std::max<int64_t>(kr, 0));
     }
@@ -402,15 +392,23 @@ template <size_t... I>
 constexpr std::array<Gf8Fn, sizeof...(I)> make_gf8_table(std::index_sequence<I...>) {
     return {{&run_gf8<int(I / kMaxRows) + 1, int(I % kMaxRows) + 1>...}};
 }
-const auto kGf8Table = make_gf8_table(std::make_index_sequence<kMaxSrc * kMaxRows>{});
+const auto kGf8Table = make_gf8_table(std::make_index_sequence<kMaxK * kMaxRows>{});
+
+using Gf8MgFn = hipError_t (*)(const Gf8MgLaunch &, hipStream_t);
+
+template <size_t... I>
+constexpr std::array<Gf8MgFn, sizeof...(I)> make_gfm_table(std::index_sequence<I...>) {
+    return {{&run_gf8_mg<int(I / 2) + 1, int(I % 2) + 3>...}};
+}
+const auto kGfmTable = make_gfm_table(std::make_index_sequence<kMaxK * 2>{});
 
 using BmFn = hipError_t (*)(const BmLaunch &, hipStream_t);
 
 template <size_t... I>
 constexpr std::array<BmFn, sizeof...(I)> make_bm_table(std::index_sequence<I...>) {
-    return {{&run_bm<int(I / kMaxRows) + 1, int(I % kMaxRows) + 1>...}};
+    return {{&run_bm<int(I / kMaxBmOut) + 1, int(I % kMaxBmOut) + 1>...}};
 }
-const auto kBmTable = make_bm_table(std::make_index_sequence<8 * kMaxRows>{});
+const auto kBmTable = make_bm_table(std::make_index_sequence<8 * kMaxBmOut>{});
 
 using GatherFn = hipError_t (*)(const GatherLaunch &, hipStream_t);
 
@@ -418,7 +416,7 @@ template <size_t... I>
 constexpr std::array<GatherFn, sizeof...(I)> make_gg8_table(std::index_sequence<I...>) {
     return {{&run_gf8_gather<int(I / kMaxRows) + 1, int(I % kMaxRows) + 1>...}};
 }
-const auto kGg8Table = make_gg8_table(std::make_index_sequence<kMaxSrc * kMaxRows>{});
+const auto kGg8Table = make_gg8_table(std::make_index_sequence<kMaxK * kMaxRows>{});
 
 template <size_t... I>
 constexpr std::array<GatherFn, sizeof...(I)> make_gbm_table(std::index_sequence<I...>) {
@@ -481,21 +479,43 @@ uint32_t stream_blocks(uint64_t len) {
 }  // namespace
 
 hipError_t launch_gf8(const Gf8Launch &L, hipStream_t stream) {
-    if (L.k < 1 || L.k > kMaxSrc || L.rows < 1 || L.rows > kMaxRows) return hipErrorInvalidValue;
+    if (L.k < 1 || L.k > kMaxK || L.rows < 1 || L.rows > kMaxRows) return hipErrorInvalidValue;
     if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
     if (L.len / 16 > uint64_t(UINT32_MAX)) return hipErrorInvalidValue;
     return kGf8Table[size_t(L.k - 1) * kMaxRows + size_t(L.rows - 1)](L, stream);
 }
 
+hipError_t launch_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
+    if (L.k < 1 || L.k > kMaxK || L.rows <= kMaxRows || L.rows > kMaxSrc || !L.tabs || L.len % 16) return hipErrorInvalidValue;
+    if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
+    if (L.len / 16 > uint64_t(UINT32_MAX)) return hipErrorInvalidValue;
+    return kGfmTable[size_t(L.k - 1) * 2 + size_t(gf8_mg_rows(L.rows) - 3)](L, stream);
+}
+
+void gf8_mg_tables(const uint8_t *coef, int rows, int k, std::vector<uint32_t> &out) {
+    const int R = gf8_mg_rows(rows), groups = (rows + R - 1) / R;
+    out.assign(size_t(groups) * R * k * 8, 0u);
+    for (int r = 0; r < rows; ++r)
+        for (int j = 0; j < k; ++j) {
+            const Gf8Coef c = gf8_coef(coef[size_t(r) * k + j]);
+            uint32_t *t = &out[(size_t(r) * k + j) * 8];
+            t[0] = c.t0;
+            t[1] = c.t1;
+            t[2] = c.u0;
+            t[3] = c.u1;
+            t[4] = c.v;
+        }
+}
+
 hipError_t launch_bm(const BmLaunch &L, hipStream_t stream) {
-    if (L.k < 1 || L.k > kMaxSrc || L.rows < 1 || L.rows > kMaxRows || L.w < 1 || L.w > 8)
+    if (L.k < 1 || L.k > kMaxK || L.rows < 1 || L.rows > (L.stab ? kMaxRows : kMaxBmOut) || L.w < 1 || L.w > 8)
         return hipErrorInvalidValue;
     if (L.packet == 0 || L.n_stripes == 0) return hipSuccess;
-    return kBmTable[size_t(L.w - 1) * kMaxRows + size_t(L.rows - 1)](L, stream);
+    return kBmTable[size_t(L.w - 1) * kMaxBmOut + size_t(L.rows - 1)](L, stream);
 }
 
 hipError_t launch_gf8_gather(const GatherLaunch &L, hipStream_t stream) {
-    if (L.k < 1 || L.k > kMaxSrc || L.rows < 1 || L.rows > kMaxRows || !L.stab || !L.dtab || !L.desc)
+    if (L.k < 1 || L.k > kMaxK || L.rows < 1 || L.rows > kMaxRows || !L.stab || !L.dtab || !L.desc)
         return hipErrorInvalidValue;
     if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
     if (L.len / 16 > uint64_t(UINT32_MAX)) return hipErrorInvalidValue;
@@ -503,7 +523,7 @@ hipError_t launch_gf8_gather(const GatherLaunch &L, hipStream_t stream) {
 }
 
 hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream) {
-    if (L.k < 1 || L.k > kMaxSrc || L.rows < 1 || L.rows > kMaxRows || L.w < 1 || L.w > 8 || !L.stab || !L.dtab ||
+    if (L.k < 1 || L.k > kMaxK || L.rows < 1 || L.rows > kMaxRows || L.w < 1 || L.w > 8 || !L.stab || !L.dtab ||
         !L.desc)
         return hipErrorInvalidValue;
     if (L.len == 0 || L.n_stripes == 0) return hipSuccess;

@@ -4,12 +4,15 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace mec {
 
-constexpr int kMaxSrc = 32;   // k <= 32 (RS_N_MAX)
-constexpr int kMaxRows = 4;   // outputs per launch; more are split into groups
-constexpr int kMaxBmRows = 32;
+constexpr int kMaxSrc = 32;   // k + m <= 32 (RS_N_MAX)
+constexpr int kMaxK = 31;     // sources of one launch: k <= 31 (m >= 1)
+constexpr int kMaxRows = 4;   // outputs per launch; more are split into groups (gf8: see gf8_mg_kernel)
+constexpr int kMaxBmOut = 8;  // outputs per strided bitmatrix launch (m > 8 splits)
+constexpr int kMaxBmRows = kMaxBmOut * 8;  // its output packets (outputs x w)
 
 // One GF(2^8) coefficient c as the three byte-permute tables used on the
 // device: bits 0-2 of a byte index {t1:t0} = c*{0..7}; bits 3-5 index
@@ -57,8 +60,8 @@ struct BmLaunch {
     const uint64_t *stab, *dtab;
     uint32_t sstride, dstride;
     int64_t src_off[kMaxSrc];
-    int64_t dst_off[kMaxRows];
-    int k, rows, w;        // rows = output chunks (each w packets)
+    int64_t dst_off[kMaxBmOut];
+    int k, rows, w;        // rows = output chunks (each w packets), <= kMaxRows when gathered
     uint64_t packet;
     uint32_t n_stripes;
     bool accumulate;
@@ -100,7 +103,33 @@ struct GatherLaunch {
     bool accumulate;       // XOR into outputs
 };
 
+// Host side of a multi-group launch: rows (> kMaxRows) outputs at dst_off,
+// coef[r * k + j]; the permute tables in device memory (tabs, from
+// gf8_mg_tables for the same coef and R = gf8_mg_rows(rows)).
+struct Gf8MgLaunch {
+    const uint8_t *src;
+    uint8_t *dst;
+    int64_t src_stripe_stride, dst_stripe_stride;
+    int64_t src_off[kMaxSrc];
+    int64_t dst_off[kMaxSrc];
+    int k, rows;
+    uint64_t len;
+    uint32_t n_stripes;
+    bool accumulate, vand;
+    const uint32_t *tabs;
+};
+// Rows per group: 3 or 4, whichever pads fewer rows (5 -> 3+2, 6 -> 3+3,
+// 7 -> 4+3, 8 -> 4+4, 9 -> 3+3+3).
+inline int gf8_mg_rows(int rows) {
+    const int g4 = (rows + 3) / 4, g3 = (rows + 2) / 3;
+    return g4 * 4 - rows <= g3 * 3 - rows ? 4 : 3;
+}
+// The permute-table image for coef (rows x k) at R rows per group: groups x
+// R x k x 8 dwords, padding rows zero.
+void gf8_mg_tables(const uint8_t *coef, int rows, int k, std::vector<uint32_t> &out);
+
 hipError_t launch_gf8(const Gf8Launch &L, hipStream_t stream);
+hipError_t launch_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream);
 hipError_t launch_gf8_gather(const GatherLaunch &L, hipStream_t stream);
 hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream);
 hipError_t launch_bm(const BmLaunch &L, hipStream_t stream);

@@ -26,12 +26,6 @@ struct Knobs {
             if (unset) {
                 put(kKnobSgroup, kKnobUnset);
                 put(kKnobSrun, kKnobUnset);
-            } else if (value[0] == 'x') {
-                put(kKnobSgroup, kKnobXcd);
-                put(kKnobSrun, kKnobUnset);
-            } else if (value[0] == 'p') {
-                put(kKnobSgroup, kKnobPerm);
-                put(kKnobSrun, value[1] ? int64_t(std::atoll(value + 1)) : kKnobUnset);
             } else {
                 put(kKnobSgroup, num);
                 const char *c = std::strchr(value, ':');

@@ -13,7 +13,7 @@ namespace mec {
 namespace detail {
 
 enum Knob : int {
-    kKnobSgroup = 0,  // MEC_SGROUP=<group>[:<run>] | x | p[<mult>]  (kKnobXcd / kKnobPerm)
+    kKnobSgroup = 0,  // MEC_SGROUP=<group>[:<run>]
     kKnobSrun,        //   ... its run length
     kKnobWindows,     // MEC_WINDOWS=<n>
     kKnobBlock,       // MEC_BLOCK=64|256
@@ -25,8 +25,6 @@ enum Knob : int {
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;
-constexpr int64_t kKnobXcd = -2;   // MEC_SGROUP=x
-constexpr int64_t kKnobPerm = -3;  // MEC_SGROUP=p[<mult>]
 
 // Current value, or kKnobUnset.
 int64_t knob(Knob k);

@@ -45,6 +45,33 @@ void bit_block(const Field &f, unsigned e, uint32_t w, uint8_t *mask, size_t mst
     }
 }
 
+// The device copy of coef's multi-group permute tables (gf8_mg_kernel),
+// uploaded at first use and kept for the context's lifetime.
+int mg_tables(mec_ctx *c, const Mat &coef, size_t rows, size_t ns, const uint32_t *&out) {
+    std::string key(reinterpret_cast<const char *>(coef.data()), rows * ns);
+    key += char(rows);
+    key += char(ns);
+    std::lock_guard<std::mutex> g(c->mg_mu);
+    auto it = c->mg_tabs.find(key);
+    if (it != c->mg_tabs.end()) {
+        out = it->second;
+        return MEC_OK;
+    }
+    std::vector<uint32_t> img;
+    mec::gf8_mg_tables(coef.data(), int(rows), int(ns), img);
+    uint32_t *d = nullptr;
+    DeviceGuard dg(c->device);
+    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), img.size() * sizeof(uint32_t)));
+    const hipError_t e = hipMemcpy(d, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return hip_fail(e, "mg tables");
+    }
+    c->mg_tabs.emplace(key, d);
+    out = d;
+    return MEC_OK;
+}
+
 // outputs (^)= coef (nd x ns over GF(2^w)) * sources, every stripe.
 int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bool accumulate, hipStream_t stream) {
     const size_t ns = lay.ns, nd = lay.nd;
@@ -56,8 +83,33 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
                 HIP_TRY(hipMemsetAsync(lay.dst + int64_t(s) * lay.dss + lay.dst_off[r], 0, c->cs, stream));
         return MEC_OK;
     }
-    for (size_t r0 = 0; r0 < nd; r0 += mec::kMaxRows) {
-        const int rows = int(std::min<size_t>(mec::kMaxRows, nd - r0));
+    const bool probe = c->probe.load(std::memory_order_relaxed) == MEC_PROBE_XOR;
+    if (c->byte_wise() && nd > size_t(mec::kMaxRows) && c->cs % 16 == 0 && !probe) {
+        // more than 4 outputs: one pass over the sources (gf8_mg_kernel)
+        mec::Gf8MgLaunch L{};
+        L.src = lay.src;
+        L.dst = lay.dst;
+        L.src_stripe_stride = lay.sss;
+        L.dst_stripe_stride = lay.dss;
+        L.k = int(ns);
+        L.rows = int(nd);
+        L.len = c->cs;
+        L.n_stripes = n_stripes;
+        L.accumulate = accumulate;
+        for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
+        for (size_t r = 0; r < nd; ++r) L.dst_off[r] = lay.dst_off[r];
+        bool vand = true;  // row 0 and column 0 all ones (Jerasure / ISA-L RS parity rows)
+        for (size_t j = 0; j < ns && vand; ++j) vand = coef[j] == 1;
+        for (size_t r = 0; r < nd && vand; ++r) vand = coef[r * ns] == 1;
+        L.vand = vand;
+        int rc = mg_tables(c, coef, nd, ns, L.tabs);
+        if (rc != MEC_OK) return rc;
+        HIP_TRY(mec::launch_gf8_mg(L, stream));
+        return MEC_OK;
+    }
+    const size_t step = c->byte_wise() ? size_t(mec::kMaxRows) : size_t(mec::kMaxBmOut);
+    for (size_t r0 = 0; r0 < nd; r0 += step) {
+        const int rows = int(std::min<size_t>(step, nd - r0));
         if (c->byte_wise()) {
             mec::Gf8Launch L{};
             L.src = lay.src;
@@ -69,7 +121,7 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
             L.len = c->cs;
             L.n_stripes = n_stripes;
             L.accumulate = accumulate;
-            L.probe = c->probe.load(std::memory_order_relaxed) == MEC_PROBE_XOR;
+            L.probe = probe;
             for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
             for (int i = 0; i < rows; ++i) L.dst_off[i] = lay.dst_off[r0 + i];
             for (int i = 0; i < rows; ++i)
@@ -348,6 +400,7 @@ void mec_destroy(mec_ctx *c) {
             }
             if (c->bdev[i]) (void)hipFree(c->bdev[i]);
         }
+        for (auto &t : c->mg_tabs) (void)hipFree(t.second);
     }
     delete c;
 }
@@ -448,6 +501,8 @@ int mec_set_probe(mec_ctx *c, int mode) {
     if (mode == MEC_PROBE_XOR && !c->byte_wise())
         return fail(MEC_EINVAL, "the XOR twin exists for byte-wise families only");
     c->probe.store(mode, std::memory_order_relaxed);
+    // a multi-device context launches on its shards
+    for (mec_ctx *sh : c->shards) sh->probe.store(mode, std::memory_order_relaxed);
     return MEC_OK;
 }
 

@@ -290,7 +290,20 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                     c = 1;
                     break;
                 }
-                if (lf == epoch) break;  // part 0 has left and every job it took has run here
+                if (lf == epoch) {
+                    // part 0 has left: `left` was stored (release) after its
+                    // last `go`, so acquire and read `go` once more — the two
+                    // relaxed loads above are not ordered, and a stale `go`
+                    // seen with the new `left` would skip part 0's last job
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    const uint64_t q2 = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (q2 > last) {
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                        last = q2;
+                        c = 1;
+                    }
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(2);
             }
             cmd = c;
@@ -410,15 +423,17 @@ int queue_revive(mec_ctx *c, HostQueue *q) {
     return queue_launch(c, q);
 }
 
-// Wait up to `ms` for the resident grid to leave; true once it has.
-bool queue_drained(HostQueue *q, int ms) {
+// Wait up to `ms` for the resident grid to leave.
+enum class Drain { kLeft, kFailed, kRunning };
+Drain queue_drained(HostQueue *q, int ms) {
     const auto t0 = std::chrono::steady_clock::now();
-    while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(ms)) {
+    for (;;) {
         const hipError_t e = hipStreamQuery(q->stream);
-        if (e != hipErrorNotReady) return true;  // finished (or failed: either way no longer running)
+        if (e == hipSuccess) return Drain::kLeft;
+        if (e != hipErrorNotReady) return Drain::kFailed;  // the grid faulted: its outputs are unknown
+        if (std::chrono::steady_clock::now() - t0 >= std::chrono::milliseconds(ms)) return Drain::kRunning;
         std::this_thread::sleep_for(std::chrono::microseconds(200));
     }
-    return false;
 }
 
 }  // namespace
@@ -430,7 +445,13 @@ void queue_stop(mec_ctx *c) {
     {
         DeviceGuard dg(c->device);
         __atomic_store_n(q->ctl_host + kQCtlStop, 1u, __ATOMIC_RELEASE);
-        (void)hipStreamSynchronize(q->stream);  // every workgroup sees the stop word and returns
+        // every workgroup sees the stop word within one poll interval; a grid
+        // still running after the cap (a hung job) keeps its memory: freeing
+        // slots and control words under a running kernel would fault it
+        if (queue_drained(q, int(std::max<uint64_t>(q->timeout_ms, 1000))) == Drain::kRunning) {
+            fprintf(stderr, "libmec: host queue kernel still running at mec_destroy; its memory is leaked\n");
+            return;
+        }
         (void)hipStreamDestroy(q->stream);
         (void)hipHostFree(q->host);
         (void)hipFree(q->act);
@@ -583,28 +604,39 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
                 // Withdraw the job (seq moves back: a part 0 that has not
                 // taken it never will; once taken, every part runs the
                 // unchanged descriptor to the end), stop the queue for good,
-                // and wait for the whole grid to leave — however long that
-                // takes: until then a part may still write the caller's
-                // chunks.  Then done[0] == seq means the job ran (the other
-                // parts leave only after part 0, with its jobs done);
-                // otherwise nothing touched the chunks and the launch path
-                // codes them instead.
-                rc = MEC_OK;
+                // and wait for the whole grid to leave, at most
+                // kQDrainFactor x the call timeout.  Then: every part's done
+                // word == seq -> the job ran, MEC_OK; none -> nothing touched
+                // the chunks and the launch path codes them (taken = false);
+                // some, a faulted grid, or a grid still running at the cap ->
+                // MEC_EHIP with the slot left busy (its outputs are partial or
+                // may still be written; an accumulate job must not be run
+                // again on top of the parts that applied it).
                 if (dt > std::chrono::milliseconds(q->timeout_ms)) q->timeouts++;
                 __atomic_store_n(&s->seq, seq - 1, __ATOMIC_SEQ_CST);
                 q->broken.store(true);
                 __atomic_store_n(q->ctl_host + kQCtlStop, 1u, __ATOMIC_RELEASE);
-                for (int waited = 0; !queue_drained(q, 5000); waited += 5)
-                    fprintf(stderr, "libmec: host queue stopped after a %llu ms call timeout; waiting for the "
-                                    "resident kernel to leave (%d s)\n",
-                            (unsigned long long)q->timeout_ms, waited + 5);
-                if (__atomic_load_n(&s->done[0], __ATOMIC_ACQUIRE) != seq) taken = false;  // never ran
+                const Drain dr = queue_drained(
+                    q, int(std::min<uint64_t>(std::max<uint64_t>(kQDrainFactor * q->timeout_ms, 10000), 600000)));
+                uint32_t ran = 0;
+                for (uint32_t p = 0; p < q->parts; ++p) ran += __atomic_load_n(&s->done[p], __ATOMIC_ACQUIRE) == seq;
+                if (dr == Drain::kLeft && ran == q->parts) {
+                    rc = MEC_OK;
+                } else if (dr == Drain::kLeft && ran == 0) {
+                    rc = MEC_OK;
+                    taken = false;  // never ran: the launch path takes the call
+                } else {
+                    rc = fail(MEC_EHIP, "host queue call timed out after %llu ms and the resident kernel %s "
+                                        "(%u of %u parts finished); the outputs are undefined",
+                              (unsigned long long)q->timeout_ms,
+                              dr == Drain::kFailed ? "faulted" : dr == Drain::kRunning ? "did not leave" : "left",
+                              ran, q->parts);
+                }
                 break;
             }
             if (dt > std::chrono::microseconds(200)) std::this_thread::yield();
             if (queue_revive(c, q) != MEC_OK && !q->broken.load()) {
-                rc = MEC_EHIP;  // the relaunch failed (error text set); the job is withdrawn below
-                q->broken.store(true);
+                q->broken.store(true);  // the relaunch failed: the next pass withdraws the job
             }
         }
         __builtin_ia32_pause();

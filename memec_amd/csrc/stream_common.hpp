@@ -97,28 +97,11 @@ __device__ __forceinline__ uint32_t block_order(uint32_t win) {
 // stripe of the group the next 8 tiles.  group = 0 keeps the identity map;
 // tiles % run == 0 and run % 8 == 0 whenever group != 0 (host side,
 // stripe_group; `run` consecutive tiles per stripe visit, default 8).
-constexpr uint32_t kXcdRegions = 0xffffffffu;  // stripe_group value of MEC_SGROUP=x
-// stripe_group value of MEC_SGROUP=p[<mult>] (experiment): block q-th
-// stripe visit goes to stripe (q * run) mod ns, run coprime to ns, so the
-// blocks resident at once work on stripes scattered over the whole buffer
-constexpr uint32_t kStripePerm = 0xfffffffeu;
 __device__ __forceinline__ void stripe_tile(uint32_t bid, uint32_t tiles, uint32_t ns, uint32_t group, uint32_t run,
                                             uint32_t &stripe, uint32_t &tile) {
     if (group == 0) {
         stripe = bid / tiles;
         tile = bid - stripe * tiles;
-        return;
-    }
-    if (group == kStripePerm) {
-        const uint32_t q = bid / tiles;
-        tile = bid - q * tiles;
-        stripe = uint32_t((uint64_t(q) * run) % ns);
-        return;
-    }
-    if (group == kXcdRegions) {  // experiment: XCD x (block id mod 8) takes the x-th eighth of each stripe
-        stripe = bid / tiles;
-        const uint32_t r = bid - stripe * tiles;
-        tile = (r & 7) * (tiles >> 3) + (r >> 3);
         return;
     }
     const uint32_t per = group * tiles;
@@ -130,7 +113,9 @@ __device__ __forceinline__ void stripe_tile(uint32_t bid, uint32_t tiles, uint32
 }
 // Host: stripes per group for a strided launch of `tiles` blocks per stripe
 // (0 = identity) and the run length.  MEC_SGROUP=<n>[:<run>] overrides
-// (experiments flip it).
+// (experiments flip it).  (Round 3's experiment-only maps — every eighth
+// tile per XCD, a stripe permutation — measured worse and were removed from
+// the product kernels)
 uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool in_place, bool bitmatrix,
                       uint32_t &run);
 
@@ -144,6 +129,16 @@ uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int6
 // one-wave blocks and the split wave caps; kernels.hip).
 uint32_t bm_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span, uint64_t chunk, int rows,
                     int k);
+
+// Template instantiation lists: X(K, R) for every source count a launch can
+// have (k + m <= 32 with m >= 1, so K <= kMaxK), split in two halves so the
+// units build in parallel; kernels.hip declares the same lists `extern` so
+// its dispatch tables do not instantiate a second copy.
+#define MEC_FOR_K_LO(X, R) \
+    X(1, R) X(2, R) X(3, R) X(4, R) X(5, R) X(6, R) X(7, R) X(8, R) X(9, R) X(10, R) X(11, R) X(12, R) X(13, R) X(14, R) X(15, R) X(16, R)
+#define MEC_FOR_K_HI(X, R) \
+    X(17, R) X(18, R) X(19, R) X(20, R) X(21, R) X(22, R) X(23, R) X(24, R) X(25, R) X(26, R) X(27, R) X(28, R) X(29, R) X(30, R) X(31, R)
+#define MEC_FOR_K(X, R) MEC_FOR_K_LO(X, R) MEC_FOR_K_HI(X, R)
 
 // ---------------------------------------------------------------------------
 // partial (tail) units: < 16 bytes at the end of a region

@@ -156,7 +156,7 @@ def test_knobs_through_the_api_not_the_environment():
     changes them at run time (no getenv on a launch path) and refuses
     unknown names."""
     import memec_amd
-    for name, value in (("MEC_WPC", "12"), ("MEC_SGROUP", "x"), ("MEC_SGROUP", "16:8"), ("MEC_BLOCK", "256"),
+    for name, value in (("MEC_WPC", "12"), ("MEC_SGROUP", "0"), ("MEC_SGROUP", "16:8"), ("MEC_BLOCK", "256"),
                         ("MEC_BM_VW", "2"), ("MEC_GBLOCK", "64"), ("MEC_GWPC", "0"), ("MEC_WINDOWS", "2"),
                         ("MEC_COPY_THREADS", "4")):
         memec_amd.set_knob(name, value)

@@ -185,3 +185,20 @@ def test_configs0_reference_cpu_leg():
     assert r["kind"] == "reference" and r["cores"] == 1
     assert r["encode_value"] > 0 and r["decode_value"] > 0
     assert r["encode_matches_oracle"] is True and r["decode_restores_codewords"] is True
+
+
+def test_cpu_legs_run_on_rank0_at_every_world_size():
+    """The reference CPU baseline is in every line rank 0 prints — at N = 1,
+    2, 4 and 8 — and every CPU leg (cpu_baseline, the decode twin's, configs[0]'s
+    reference_cpu, the samples they take) is gated by that one rule, after
+    the barrier that ends every rank's GPU legs."""
+    import inspect
+    for world in (1, 2, 4, 8):
+        assert bench.runs_cpu_legs(0, world, False) is True
+        assert bench.runs_cpu_legs(0, world, True) is False
+        for r in range(1, world):
+            assert bench.runs_cpu_legs(r, world, False) is False
+    src = inspect.getsource(bench.main)
+    assert "world == 1" not in src
+    assert src.count("runs_cpu_legs(rank, world, args.no_cpu_baseline)") == 5
+    assert src.index("dist.barrier()") < src.index("threads, host = host_cores()")

@@ -14,11 +14,11 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(*extra):
+def _run(*extra, gpus=2):
     env = dict(os.environ, MEC_BENCH_DIST_BACKEND="gloo")
     for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(v, None)
-    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--steps", "3",
                           "--warmup", "1", "--no-ceiling", *extra],
                          env=env, capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -34,7 +34,11 @@ def test_bench_gpus2_spawns_ranks_weak():
     assert rec["config"]["global_stripes"] == 128 and rec["config"]["stripes_per_gpu"] == 64
     assert rec["decode"]["verified"] is True
     assert rec["value"] > 0 and rec["roofline"]["kernel_ms"] > 0
-    assert rec["cpu_baseline"] is None  # rank 0 at N=1 only
+    # the reference CPU path beside the N = 2 line too (rank 0, after the GPU legs)
+    cb = rec["cpu_baseline"]
+    assert cb["kind"] == "reference" and cb["matches_gpu"] is True and cb["value"] > 0, cb
+    assert rec["decode"]["cpu_baseline"]["kind"] == "reference"
+    assert rec["decode"]["cpu_baseline"]["matches_gpu"] is True
 
 
 @pytest.mark.timeout(500)
@@ -51,7 +55,8 @@ def test_bench_gpus2_default_line_rehearsal():
     c0 = rec["other_configs"]["configs[0]"]
     assert c0["stripes_per_gpu"] == 65536 and c0["global_stripes"] == 131072 and c0["parity"]["equal"] is True
     assert c0["decode"]["verified"] is True and c0["decode"]["parity"]["equal"] is True
-    assert "reference_cpu" not in c0  # the CPU leg runs at N = 1 only
+    assert c0["reference_cpu"]["value"] > 0  # the reference's own configs[0] CPU path at N = 2 too
+    assert rec["cpu_baseline"]["kind"] == "reference" and rec["cpu_baseline"]["matches_gpu"] is True
     c3, c4 = rec["other_configs"]["configs[3]"], rec["other_configs"]["configs[4]"]
     assert c3["stripes_per_gpu"] == 65536 and c3["global_stripes"] == 131072
     assert c3["verified"] is True and c3["parity"]["equal"] is True and c3["decode_parity"]["equal"] is True
@@ -61,7 +66,7 @@ def test_bench_gpus2_default_line_rehearsal():
 
 
 def test_bench_gpus2_strong_crs():
-    rec = _run("--config", "crs_enc", "--strong", "--stripes", "96")
+    rec = _run("--config", "crs_enc", "--strong", "--stripes", "96", "--no-cpu-baseline")
     assert rec["n_gpus"] == 2 and rec["scaling"] == "strong"
     assert rec["config"]["global_stripes"] == 96 and rec["config"]["stripes_per_gpu"] == 48
     assert rec["decode"]["verified"] is True
@@ -90,3 +95,14 @@ def test_bench_under_launcher_uses_rccl():
     assert rec["decode"]["verified"] is True
     assert rec["other_configs"]["configs[3]"]["verified"] is True
     assert rec["other_configs"]["configs[4]"]["decode"]["verified"] is True
+
+
+@pytest.mark.timeout(500)
+def test_bench_gpus4_carries_cpu_baseline():
+    """N = 4 (four gloo ranks on the one GPU): the line rank 0 prints carries
+    the reference CPU baseline, checked against rank 0's GPU parity."""
+    rec = _run("--stripes", "32", gpus=4)
+    assert rec["n_gpus"] == 4 and rec["dist"]["world_size"] == 4
+    cb = rec["cpu_baseline"]
+    assert cb["kind"] == "reference" and cb["matches_gpu"] is True and cb["cores"] >= 1, cb
+    assert "rank 0 of 4" in cb["when"]

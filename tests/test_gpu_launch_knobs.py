@@ -138,7 +138,7 @@ def _stripes_km(fam, k, m, cs, n, seed):
     return base
 
 
-@pytest.mark.parametrize("group", ["0", "3:8", "7:16", "4:64", "64:8", "bad:7", "p", "p7", "p10", "x"])
+@pytest.mark.parametrize("group", ["0", "3:8", "7:16", "4:64", "64:8", "bad:7"])
 def test_stripe_group_overrides(group, knobs):
     """The stripe-group block map (stream_common.hpp stripe_tile) with
     forced groups and run lengths, a last group shorter than the rest

@@ -366,6 +366,44 @@ def test_queue_timeout_withdraws_and_falls_back(fam):
         slab.close()
 
 
+@pytest.mark.parametrize("fam", ["rs", "cauchy"])
+def test_queue_timeout_multipart_all_or_nothing(fam):
+    """the timeout path on a multi-part slot (64 KiB
+    chunks: 4 workgroups per slot).  After the withdrawal the caller checks
+    every part's done word: all -> the job ran, none -> the launch path codes
+    it; so encodes and accumulating delta updates (which must not be applied
+    twice) stay exact whichever way each call went."""
+    k, m, cs = 6, 3, 65536
+    os.environ["MEC_QUEUE_TIMEOUT_MS"] = "0"
+    slab = Slab(k + m + 1, cs, 93)
+    c = Codec(fam, k, m, cs)
+    try:
+        c.set_host_queue(4)
+        assert c.stats()["queue_parts"] == 4
+        data = [slab.view(j).copy() for j in range(k)]
+        want = O.encode(fam, k, m, [d.copy() for d in data], cs)
+        for i in range(m):
+            slab.view(k + i)[:] = 0
+            encode_index(c, slab, k, list(range(k)), k + i, i + 1)
+            assert np.array_equal(slab.view(k + i), want[i]), i
+        # accumulate: parity ^= A[:, 2] * delta, twice -> back to `want`, and
+        # once more -> the encode of data with column 2 ^= delta
+        delta = slab.view(k + m)
+        for rnd in range(3):
+            c.encode_update_host(2, delta, [slab.view(k + i) for i in range(m)])
+        d2 = [d.copy() for d in data]
+        d2[2] ^= delta
+        want2 = O.encode(fam, k, m, d2, cs)
+        for i in range(m):
+            assert np.array_equal(slab.view(k + i), want2[i]), i
+        st = c.stats()
+        assert st["queue_broken"] and st["queue_timeouts"] >= 1
+    finally:
+        os.environ.pop("MEC_QUEUE_TIMEOUT_MS", None)
+        c.close()
+        slab.close()
+
+
 def test_queue_fallbacks():
     """Calls the queue does not serve still code correctly through launches."""
     k, m = 4, 2
