@@ -41,6 +41,11 @@ CONFIGS = {
     # A[:, j] * delta for one data column j (last field = j)
     "rs8_update": ("rs", 8, 2, 4096, 65536, "update", 3),
     "rs_update": ("rs", 10, 4, 1 << 20, 4096, "update", 3),
+    # wide codes (m > 4, k + m <= 32: rscoding.cc:26-29): one pass over the
+    # sources for every parity (gf8_mg_kernel)
+    "rs16_8": ("rs", 16, 8, 65536, 16384, "encode", None),
+    "rs16_8_dec": ("rs", 16, 8, 65536, 16384, "decode", [0, 1, 2, 3, 4, 5, 6, 7]),
+    "isal12_8": ("isal_rs", 12, 8, 65536, 16384, "encode", None),
 }
 WORKLOAD_NAMES = {
     "rs_enc": "RS(10,4) encode, 1 MiB chunks, 4096 stripes per GPU (BASELINE configs[1])",
@@ -53,6 +58,9 @@ WORKLOAD_NAMES = {
     "rs42_dec": "RS(4,2) decode 2 erasures {0,1}, 4 KiB chunks, 65536 stripes per GPU (configs[0] shape)",
     "rs8_update": "RS(8,2) delta update of data column 3 into both parities, 4 KiB chunks, 65536 stripes per GPU",
     "rs_update": "RS(10,4) delta update of data column 3 into all 4 parities, 1 MiB chunks, 4096 stripes per GPU",
+    "rs16_8": "RS(16,8) encode, 64 KiB chunks, 16384 stripes per GPU (wide code, one pass)",
+    "rs16_8_dec": "RS(16,8) decode 8 erasures {0..7}, 64 KiB chunks, 16384 stripes per GPU (wide code)",
+    "isal12_8": "ISA-L RS(12,8) encode, 64 KiB chunks, 16384 stripes per GPU (wide code, one pass)",
 }
 
 

@@ -15,7 +15,7 @@ struct Knobs {
     Knobs() {
         for (auto &x : v) x.store(kKnobUnset, std::memory_order_relaxed);
         for (const char *n : {"MEC_SGROUP", "MEC_WINDOWS", "MEC_BLOCK", "MEC_GBLOCK", "MEC_GWPC", "MEC_BM_VW",
-                              "MEC_WPC", "MEC_COPY_THREADS"})
+                              "MEC_WPC", "MEC_COPY_THREADS", "MEC_WIDE"})
             apply(n, std::getenv(n));
     }
     bool apply(const char *name, const char *value) {
@@ -38,7 +38,7 @@ struct Knobs {
             Knob k;
         } kPlain[] = {{"MEC_WINDOWS", kKnobWindows}, {"MEC_BLOCK", kKnobBlock},   {"MEC_GBLOCK", kKnobGblock},
                       {"MEC_GWPC", kKnobGwpc},       {"MEC_BM_VW", kKnobBmVw},     {"MEC_WPC", kKnobWpc},
-                      {"MEC_COPY_THREADS", kKnobCopyThreads}};
+                      {"MEC_COPY_THREADS", kKnobCopyThreads}, {"MEC_WIDE", kKnobWide}};
         for (const auto &p : kPlain)
             if (!std::strcmp(name, p.name)) {
                 put(p.k, num);

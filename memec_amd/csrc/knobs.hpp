@@ -22,6 +22,7 @@ enum Knob : int {
     kKnobBmVw,        // MEC_BM_VW=2|4
     kKnobWpc,         // MEC_WPC=<waves> (0 = no cap)
     kKnobCopyThreads, // MEC_COPY_THREADS=<n>
+    kKnobWide,        // MEC_WIDE=0: > 4 outputs as 4-row launches (A/B of gf8_mg_kernel)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

@@ -84,7 +84,8 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
         return MEC_OK;
     }
     const bool probe = c->probe.load(std::memory_order_relaxed) == MEC_PROBE_XOR;
-    if (c->byte_wise() && nd > size_t(mec::kMaxRows) && c->cs % 16 == 0 && !probe) {
+    if (c->byte_wise() && nd > size_t(mec::kMaxRows) && c->cs % 16 == 0 && !probe &&
+        mec::detail::knob(mec::detail::kKnobWide) != 0) {
         // more than 4 outputs: one pass over the sources (gf8_mg_kernel)
         mec::Gf8MgLaunch L{};
         L.src = lay.src;

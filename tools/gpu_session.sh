@@ -65,6 +65,16 @@ for step in "$@"; do
                     SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
                     --output-format csv -d "$OUT/pmc_sqlds_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --no-extra-configs --no-ceiling --steps 3 --warmup 1
             done ;;
+        wide) run wide_ab 600 python tools/wide_ab.py --steps 10 ;;
+        widepmc)
+            for sh in 0 1; do
+                for mode in wide split; do
+                    for ctr in FETCH_SIZE WRITE_SIZE; do
+                        run "pmc_wide_${sh}_${mode}_${ctr}" 300 rocprofv3 --pmc $ctr --output-format csv \
+                            -d "$OUT/pmc_wide_${sh}_${mode}_${ctr}" -o run -- python3 tools/wide_ab.py --mode $mode --shape $sh --steps 5 --warmup 1
+                    done
+                done
+            done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

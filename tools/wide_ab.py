@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""A/B of wide codes (m > 4): the one-pass multi-group kernel (gf8_mg_kernel,
+default) against 4-row launches that re-read the sources (MEC_WIDE=0).
+
+  python tools/wide_ab.py [--mode both|wide|split] [--steps N] [--pmc-out F]
+
+Every launch is checked against the other arm's parity (bit-exact), and the
+GPU time per step (HIP events around `steps` encodes / decodes) is printed
+as JSON lines.  Under `rocprofv3 --pmc FETCH_SIZE` (or WRITE_SIZE) run one
+mode only: the counter CSV then holds exactly warmup + steps coding steps
+after the fill launches, and tools/wide_ab.py --summarise sums them per step.
+"""
+import argparse
+import csv
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384, "encode"),
+          ("rs", 16, 8, 65536, 16384, "decode"), ("rs", 10, 6, 262144, 4096, "encode"),
+          ("isal_cauchy", 12, 6, 65536, 16384, "encode")]
+
+
+def run(mode, steps, warmup, shapes):
+    import torch
+    import memec_amd
+    from memec_amd import Codec, fill_random
+    torch.cuda.set_device(0)
+    out = []
+    for fam, k, m, cs, n, op in shapes:
+        c = Codec(fam, k, m, cs)
+        data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
+        fill_random(data, 1234)
+        if op == "encode":
+            par = torch.empty(n, m, cs, dtype=torch.uint8, device="cuda")
+            step = lambda: c.encode(data, par)  # noqa: E731
+            alg = (k + m) * cs * n
+            result = lambda: par  # noqa: E731
+        else:
+            st = torch.empty(n, k + m, cs, dtype=torch.uint8, device="cuda")
+            st[:, :k] = data
+            c.encode(st[:, :k], st[:, k:])
+            erased = list(range(m))
+            present = sum(1 << i for i in range(k + m) if i not in erased)
+            orig = st[:, erased].clone()
+            st[:, erased] = 0
+            step = lambda: c.decode(st, present)  # noqa: E731
+            alg = (k + m) * cs * n
+            result = lambda: st[:, erased]  # noqa: E731
+        del data
+        arms = {}
+        for arm in (["wide", "split"] if mode == "both" else [mode]):
+            memec_amd.set_knob("MEC_WIDE", None if arm == "wide" else "0")
+            for _ in range(warmup):
+                step()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(steps):
+                step()
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / steps
+            arms[arm] = {"ms_per_step": round(ms, 4), "GBps": round(alg / (ms * 1e-3) / 1e9, 1),
+                         "frac": round(alg / (ms * 1e-3) / 8e12, 4)}
+            arms[arm]["digest"] = int(result().view(torch.int64).sum().item())
+        memec_amd.set_knob("MEC_WIDE", None)
+        rec = {"family": fam, "k": k, "m": m, "chunk": cs, "stripes": n, "op": op, "alg_bytes": alg, **arms}
+        if op == "decode":
+            rec["restored"] = bool(torch.equal(result(), orig))
+        if mode == "both":
+            rec["equal"] = arms["wide"]["digest"] == arms["split"]["digest"]
+        print(json.dumps(rec), flush=True)
+        out.append(rec)
+        c.close()
+        torch.cuda.empty_cache()
+    return out
+
+
+def summarise(csv_path, counter, steps, warmup):
+    """Counter total per coding step (every gf8 kernel launch after the
+    fills, decodes' setup encode excluded by the caller's shape list)."""
+    tot, n = 0.0, 0
+    with open(csv_path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter:
+                continue
+            name = row["Kernel_Name"]
+            if "gf8" in name or "bm_kernel" in name:
+                tot += float(row["Counter_Value"])
+                n += 1
+    return tot / (steps + warmup), n
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="both", choices=["both", "wide", "split"])
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (default: all)")
+    ap.add_argument("--summarise", nargs=2, metavar=("FETCH_CSV", "WRITE_CSV"))
+    a = ap.parse_args()
+    shapes = SHAPES if a.shape < 0 else [SHAPES[a.shape]]
+    if a.summarise:
+        fam, k, m, cs, n, op = shapes[0]
+        fk, nf = summarise(a.summarise[0], "FETCH_SIZE", a.steps, a.warmup)
+        wk, nw = summarise(a.summarise[1], "WRITE_SIZE", a.steps, a.warmup)
+        rd, wr = 2 * fk * 1024, wk * 1024
+        alg_r = k * cs * n
+        alg_w = m * cs * n
+        print(json.dumps({"shape": shapes[0], "mode": a.mode, "launch_rows": [nf, nw],
+                          "read_bytes_per_step": rd, "write_bytes_per_step": wr,
+                          "read_ratio": round(rd / alg_r, 4), "write_ratio": round(wr / alg_w, 4),
+                          "traffic_ratio": round((rd + wr) / (alg_r + alg_w), 4)}))
+    else:
+        run(a.mode, a.steps, a.warmup, shapes)
