@@ -216,6 +216,9 @@ def cpu_baseline_reference(fam, k, m, cs, gpu_parity_np, seed, threads, op, eras
     import _oracle as O
 
     sample = cpu_sample(k, m, cs, threads)
+    if op != "encode":  # the GPU-encoded codewords handed over (fewer on a small --stripes run)
+        sample = min(sample, codewords.shape[0])
+        codewords = codewords[:sample]
     per = k * cs
     if op == "encode":
         data = O.fill(sample * per, seed)

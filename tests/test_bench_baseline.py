@@ -202,3 +202,18 @@ def test_cpu_legs_run_on_rank0_at_every_world_size():
     assert "world == 1" not in src
     assert src.count("runs_cpu_legs(rank, world, args.no_cpu_baseline)") == 5
     assert src.index("dist.barrier()") < src.index("threads, host = host_cores()")
+
+
+@needs_ref
+def test_reference_decode_leg_fewer_codewords_than_sample(monkeypatch):
+    """A small --stripes run hands over fewer GPU codewords than the leg's
+    sample (N = 4 x 32 stripes): the leg decodes only those (it once read
+    past them: heap corruption at exit)."""
+    monkeypatch.setattr(bench, "ref_baseline", _fast(bench.ref_baseline))
+    k, m, cs = 10, 4, 65536
+    assert bench.cpu_sample(k, m, cs, 16) > 8
+    data, par = _stripes("rs", k, m, cs, 8, 3)
+    cw = np.concatenate([data, par], axis=1)
+    r = bench.cpu_baseline_reference("rs", k, m, cs, None, 0, 16, "decode", [0, 1, 2, 3], cw)
+    assert r["kind"] == "reference" and r["matches_gpu"] is True
+    assert r["sample"].startswith("8 stripes")

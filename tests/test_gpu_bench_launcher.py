@@ -55,7 +55,7 @@ def test_bench_gpus2_default_line_rehearsal():
     c0 = rec["other_configs"]["configs[0]"]
     assert c0["stripes_per_gpu"] == 65536 and c0["global_stripes"] == 131072 and c0["parity"]["equal"] is True
     assert c0["decode"]["verified"] is True and c0["decode"]["parity"]["equal"] is True
-    assert c0["reference_cpu"]["value"] > 0  # the reference's own configs[0] CPU path at N = 2 too
+    assert c0["reference_cpu"]["encode_value"] > 0 and c0["reference_cpu"]["encode_matches_oracle"] is True
     assert rec["cpu_baseline"]["kind"] == "reference" and rec["cpu_baseline"]["matches_gpu"] is True
     c3, c4 = rec["other_configs"]["configs[3]"], rec["other_configs"]["configs[4]"]
     assert c3["stripes_per_gpu"] == 65536 and c3["global_stripes"] == 131072
