@@ -12,6 +12,12 @@
 //
 // Prints one JSON line: calls/s, data GiB/s (data bytes the calls cover),
 // and the adapter's coalescing setting (env MEMEC_GPU_COALESCE).
+//
+// Built twice from this one file: against the drop-in adapter + libmec
+// (tools/coding_bench.sh), and with -DCODING_BENCH_REF against MemEC's own
+// plugin (common/coding + Jerasure + gf_complete compiled from the
+// reference sources, oracle/Makefile `ref` -> oracle/_ref/coding_bench_ref),
+// so both sides of a comparison run the same threads, calls and chunks.
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -21,8 +27,15 @@
 #include <atomic>
 #include <vector>
 
+#ifdef CODING_BENCH_REF
+#include "common/coding/coding.hh"
+#include "common/ds/bitmask_array.hh"
+#include "common/ds/chunk_pool.hh"
+#include "common/ds/chunk_util.hh"
+#else
 #include "coding.hh"
 #include "mec.h"
+#endif
 
 static Coding *coding;
 static uint32_t K, M, CS;
@@ -50,6 +63,7 @@ static void *run(void *arg) {
     std::vector<Chunk *> c(K + M);
     char *slab = 0;
     const size_t slot = 8 + size_t(CS);
+#ifndef CODING_BENCH_REF
     if (registered) {
         // one ChunkPool-like slab per worker (slot = 8-byte header + data,
         // chunk_pool.cc:22-47), mapped for zero-copy coding
@@ -60,7 +74,9 @@ static void *run(void *arg) {
             exit(1);
         }
         for (uint32_t i = 0; i < K + M; i++) c[i] = (Chunk *)(slab + i * slot);
-    } else {
+    } else
+#endif
+    {
         for (auto &x : c) x = pool.alloc();
     }
     for (auto &x : c) {
@@ -95,10 +111,13 @@ static void *run(void *arg) {
         }
         it++;
     }
+#ifndef CODING_BENCH_REF
     if (registered) {
         mec_host_unregister(slab);
         free(slab);
-    } else {
+    } else
+#endif
+    {
         for (auto &x : c) pool.free(x);
     }
     return 0;
@@ -143,9 +162,15 @@ int main(int argc, char **argv) {
     }
     const double dt = now() - t0;
     const char *co = getenv("MEMEC_GPU_COALESCE");
-    printf("{\"bench\": \"coding_adapter\", \"scheme\": \"%s\", \"k\": %u, \"m\": %u, \"chunk\": %u, \"workers\": %d, "
+#ifdef CODING_BENCH_REF
+    const char *which = "reference";  // MemEC's own plugin, CPU
+#else
+    const char *which = "coding_adapter";
+#endif
+    printf("{\"bench\": \"%s\", \"scheme\": \"%s\", \"k\": %u, \"m\": %u, \"chunk\": %u, \"workers\": %d, "
            "\"mode\": \"%s\", \"coalesce\": %s, \"registered\": %d, \"calls_per_s\": %.1f, \"data_GiBps\": %.4f}\n",
-           argv[1], K, M, CS, W, argv[7], co ? co : "0", registered ? 1 : 0, calls / dt, bytes / dt / 1073741824.0);
+           which, argv[1], K, M, CS, W, argv[7], co ? co : "0", registered ? 1 : 0, calls / dt,
+           bytes / dt / 1073741824.0);
     Coding::destroy(coding);
     return 0;
 }

@@ -66,6 +66,7 @@ for step in "$@"; do
                     --output-format csv -d "$OUT/pmc_sqlds_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --no-extra-configs --no-ceiling --steps 3 --warmup 1
             done ;;
         wide) run wide_ab 600 python tools/wide_ab.py --steps 10 ;;
+        server) run server_pattern 900 bash tools/server_pattern.sh ;;
         widepmc)
             for sh in 0 1; do
                 for mode in wide split; do
