@@ -316,6 +316,26 @@ int mec_set_coalescing(mec_ctx *ctx, uint32_t max_batch);
  * context.  Replaces nothing in the reference: its workers call the CPU
  * plugin directly (worker.cc:128-137). */
 int mec_set_host_queue(mec_ctx *ctx, uint32_t slots);
+
+/* Latency breakdown of single-stripe queue calls (measurement only; no
+ * reference counterpart).  While enabled, part 0 of the slot that runs a
+ * call records its device clock (s_memrealtime, 100 MHz ticks) when it took
+ * the job, when the descriptor and coefficient tables were ready, and when
+ * its output stores were acknowledged; the calling thread's last such call,
+ * with its host CLOCK_MONOTONIC times of posting the job and seeing it
+ * done, is read back with mec_queue_last_trace (once; MEC_EINVAL when none
+ * is pending).  Device and host clocks are not related here: a tool
+ * calibrates the offset (tools/queue_latency.hip). */
+typedef struct {
+    uint64_t host_post_ns;  /* before the sequence-number store that posts the job */
+    uint64_t host_seen_ns;  /* when every part's done word was seen */
+    uint64_t dev_take;      /* device ticks: job taken (seq seen) */
+    uint64_t dev_desc;      /* descriptor + tables in LDS */
+    uint64_t dev_end;       /* output stores acknowledged, before the done store */
+    uint32_t parts, pad;
+} mec_queue_trace;
+int mec_queue_trace_enable(mec_ctx *ctx, int on);
+int mec_queue_last_trace(mec_queue_trace *out);
 int mec_get_stats(const mec_ctx *ctx, mec_stats *out);
 
 /* ---- measurement and experiments (no reference counterpart) --------------- */

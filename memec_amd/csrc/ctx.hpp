@@ -117,12 +117,16 @@ struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
     uint64_t pad0[15];
     uint64_t done[kQMaxParts];  // GPU -> host: number of the last job each part finished
     // sources, outputs, chunk bytes, accumulate, w (0: byte-wise GF(2^8);
-    // 1..8: Jerasure bitmatrix over w packets), packet bytes, -, -
+    // 1..8: Jerasure bitmatrix over w packets), packet bytes, trace, -
     uint32_t hdr[8];
     uint64_t src[kQMaxSrc];  // device addresses of registered chunks (0 = zeros)
     uint64_t dst[kQMaxDst];  // (0 = unwanted output)
     uint32_t coef_w[kQMaxDst * kQMaxSrc / 4];  // GF(2^8) bytes, [output][source]
     uint32_t mask_w[kQMaxSrc * kQBmRows / 4];  // bitmatrix bytes [source][output*w + l], bit x
+    // GPU -> host when hdr[6] (trace) is set: part 0's s_memrealtime when it
+    // took the job, had the descriptor and tables ready, and had its output
+    // stores acknowledged (just before its done store)
+    uint64_t trace[4];
 };
 // Grid-wide control words, after the slots in the same mapped allocation.
 enum : uint32_t { kQCtlStop = 0, kQCtlExit = 1, kQCtlWords = 2 };
@@ -142,6 +146,7 @@ struct HostQueue {
     std::atomic<bool> broken{false};  // a call timed out: the queue is stopped for good
     uint64_t idle_ticks = 0, timeout_ms = 5000;
     std::atomic<bool> *busy = nullptr;
+    std::atomic<bool> trace{false};   // mec_queue_trace_enable
     hipStream_t stream = nullptr;
     std::mutex mu;  // launches
     std::atomic<uint64_t> calls{0}, launches{0};

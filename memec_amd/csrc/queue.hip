@@ -52,6 +52,8 @@
 #include <cstring>
 #include <thread>
 
+#include <time.h>
+
 #include "ctx.hpp"
 #include "kernels.hpp"
 #include "stream_common.hpp"
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
     uint64_t *go = link + si, *left = link + nslots + si;
     const uint32_t t = threadIdx.x;
     const bool leader = blockIdx.x == 0;
-    uint64_t last = 0, t0 = 0;
+    uint64_t last = 0, t0 = 0, t_take = 0;
     if (t == 0) {
         last = sys_load(&s->done[part]);
         t0 = __builtin_amdgcn_s_memrealtime();
@@ -312,6 +314,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             for (uint32_t n = 1;; ++n) {  // one PCIe read per poll; control words every 64th
                 const uint64_t q = __hip_atomic_load(&s->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (q > last) {  // a withdrawn job moves seq back (queue_try)
+                    t_take = __builtin_amdgcn_s_memrealtime();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once per job
                     last = q;
                     c = 1;
@@ -346,6 +349,8 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
         }
         __syncthreads();
         const uint32_t ns = hdr[0], nd = hdr[1], bytes = hdr[2], acc_in = hdr[3], w = hdr[4], P = hdr[5];
+        const bool traced = hdr[6] != 0u && part == 0 && t == 0;
+        uint64_t t_desc = 0;
         if (w == 0) {  // byte-wise GF(2^8): v_perm tables from the coefficient bytes
             for (uint32_t e = t; e < nd * ns; e += nthr) {  // nthr may be 64 (one-wave parts)
                 const uint32_t r = e / ns, j = e - r * ns, b = r * kQMaxSrc + j;
@@ -358,6 +363,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                 T[4] = pack4(c, 0, 64, 128, 192);
             }
             __syncthreads();
+            if (traced) t_desc = __builtin_amdgcn_s_memrealtime();
             // this part's units: passes of nthr units, part-th of every parts
             const uint32_t full = bytes / 16, me = part * nthr + t, step = parts * nthr;
             for (uint32_t u = me; u < full; u += step)
@@ -365,6 +371,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             if (bytes % 16 && me == full % step)  // the partial last unit
                 code_unit<false>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
         } else {
+            if (traced) t_desc = __builtin_amdgcn_s_memrealtime();
             const uint32_t me = part * nthr + t, step = parts * nthr;
             switch (w) {  // uniform
                 case 1: bm_job<1>(addr, mk, ns, nd, acc_in, P, me, step); break;
@@ -387,11 +394,33 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
         // launch's own geometry; profiles/r03/host/queue_pthr_ab.log.)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (traced) {  // measurement only (mec_queue_trace_enable): vector stores before the release
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_store(&s->trace[0], t_take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&s->trace[1], t_desc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&s->trace[2], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         if (t == 0) {
             __hip_atomic_store(&s->done[part], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             if (part == 0) mark_active(act + si);
         }
     }
+}
+
+uint64_t mono_ns() {  // CLOCK_MONOTONIC, the clock mec_queue_trace reports in
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return uint64_t(ts.tv_sec) * 1000000000ull + uint64_t(ts.tv_nsec);
+}
+
+// The calling thread's last traced queue call (mec_queue_last_trace).
+struct QTrace {
+    uint64_t host_post_ns, host_seen_ns, dev_take, dev_desc, dev_end;
+    uint32_t parts, valid;
+};
+QTrace &last_trace() {
+    static thread_local QTrace t{};
+    return t;
 }
 
 uint64_t env_u64(const char *name, uint64_t dflt) {
@@ -571,6 +600,8 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     s->hdr[3] = accumulate ? 1u : 0u;
     s->hdr[4] = c->byte_wise() ? 0u : c->w;
     s->hdr[5] = c->byte_wise() ? c->cs : c->packet;
+    const bool traced = q->trace.load(std::memory_order_relaxed);
+    s->hdr[6] = traced ? 1u : 0u;
     for (size_t j = 0; j < ns; ++j) s->src[j] = addrs[j];
     for (size_t r = 0; r < nd; ++r) s->dst[r] = addrs[ns + r];
     if (c->byte_wise()) {
@@ -586,6 +617,7 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
         std::memcpy(s->mask_w, mk, sizeof(mk));
     }
     const uint64_t seq = __atomic_load_n(&s->seq, __ATOMIC_RELAXED) + 1;
+    const uint64_t t_post = traced ? mono_ns() : 0;
     __atomic_store_n(&s->seq, seq, __ATOMIC_RELEASE);  // publishes the descriptor
     // wait for the workgroup; relaunch the grid if it idled out meanwhile
     rc = MEC_OK;
@@ -641,6 +673,16 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
         }
         __builtin_ia32_pause();
     }
+    if (traced && taken && rc == MEC_OK) {
+        QTrace &tr = last_trace();
+        tr.host_seen_ns = mono_ns();
+        tr.host_post_ns = t_post;
+        tr.dev_take = s->trace[0];
+        tr.dev_desc = s->trace[1];
+        tr.dev_end = s->trace[2];
+        tr.parts = q->parts;
+        tr.valid = 1;
+    }
     q->inflight.fetch_sub(1, std::memory_order_relaxed);
     if (rc == MEC_OK && taken) {
         q->busy[i].store(false, std::memory_order_release);
@@ -655,6 +697,29 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
 using namespace mec::core;
 
 extern "C" {
+
+int mec_queue_trace_enable(mec_ctx *c, int on) {
+    CHECK_CTX(c);
+    for (mec_ctx *s : c->shards) mec_queue_trace_enable(s, on);
+    std::lock_guard<std::mutex> g(c->hq_mu);
+    if (!c->hq) return c->shards.empty() ? fail(MEC_EINVAL, "no host queue on this context") : MEC_OK;
+    c->hq->trace.store(on != 0);
+    return MEC_OK;
+}
+
+int mec_queue_last_trace(mec_queue_trace *out) {
+    if (!out) return fail(MEC_EINVAL, "null argument");
+    QTrace &t = last_trace();
+    if (!t.valid) return fail(MEC_EINVAL, "no traced queue call on this thread");
+    out->host_post_ns = t.host_post_ns;
+    out->host_seen_ns = t.host_seen_ns;
+    out->dev_take = t.dev_take;
+    out->dev_desc = t.dev_desc;
+    out->dev_end = t.dev_end;
+    out->parts = t.parts;
+    t.valid = 0;
+    return MEC_OK;
+}
 
 int mec_set_host_queue(mec_ctx *c, uint32_t slots) {
     CHECK_CTX(c);

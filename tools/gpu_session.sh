@@ -67,6 +67,12 @@ for step in "$@"; do
             done ;;
         wide) run wide_ab 600 python tools/wide_ab.py --steps 10 ;;
         server) run server_pattern 900 bash tools/server_pattern.sh ;;
+        latency)
+            for args in "rs 8 2 4096 20000 1 1" "rs 8 2 4096 20000 0 1" "rs 4 2 4096 20000 1 1" "rs 10 4 65536 5000 1 1" \
+                        "cauchy 4 2 4096 20000 1 1" "rs 8 2 4096 20000 1 2"; do
+                run "latency_$(echo $args | tr ' ' _)" 120 tools/queue_latency $args
+            done
+            grep -h '^{' "$OUT"/latency_*.log > "$OUT/latency.jsonl" ;;
         widepmc)
             for sh in 0 1; do
                 for mode in wide split; do
