@@ -321,7 +321,8 @@ int mec_set_host_queue(mec_ctx *ctx, uint32_t slots);
  * reference counterpart).  While enabled, part 0 of the slot that runs a
  * call records its device clock (s_memrealtime, 100 MHz ticks) when it took
  * the job, when the descriptor and coefficient tables were ready, and when
- * its output stores were acknowledged; the calling thread's last such call,
+ * its output stores were acknowledged (and after its acquire fence); the
+ * calling thread's last such call,
  * with its host CLOCK_MONOTONIC times of posting the job and seeing it
  * done, is read back with mec_queue_last_trace (once; MEC_EINVAL when none
  * is pending).  Device and host clocks are not related here: a tool
@@ -330,7 +331,8 @@ typedef struct {
     uint64_t host_post_ns;  /* before the sequence-number store that posts the job */
     uint64_t host_seen_ns;  /* when every part's done word was seen */
     uint64_t dev_take;      /* device ticks: job taken (seq seen) */
-    uint64_t dev_desc;      /* descriptor + tables in LDS */
+    uint64_t dev_fence;     /* its system-scope acquire fence done */
+    uint64_t dev_desc;      /* descriptor (incl. coefficient tables) in LDS */
     uint64_t dev_end;       /* output stores acknowledged, before the done store */
     uint32_t parts, pad;
 } mec_queue_trace;

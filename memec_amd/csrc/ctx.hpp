@@ -121,11 +121,16 @@ struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
     uint32_t hdr[8];
     uint64_t src[kQMaxSrc];  // device addresses of registered chunks (0 = zeros)
     uint64_t dst[kQMaxDst];  // (0 = unwanted output)
-    uint32_t coef_w[kQMaxDst * kQMaxSrc / 4];  // GF(2^8) bytes, [output][source]
-    uint32_t mask_w[kQMaxSrc * kQBmRows / 4];  // bitmatrix bytes [source][output*w + l], bit x
+    union {
+        // byte-wise: the v_perm tables of coefficient (output r, source j)
+        // at (r * sources + j) * 8 dwords (t0 t1 u0 u1 v, gf8_kernel.hpp),
+        // built on the host (a table per GF(2^8) value, computed once)
+        uint32_t tab_w[kQMaxDst * kQMaxSrc * 8];
+        uint32_t mask_w[kQMaxSrc * kQBmRows / 4];  // bitmatrix bytes [source][output*w + l], bit x
+    };
     // GPU -> host when hdr[6] (trace) is set: part 0's s_memrealtime when it
-    // took the job, had the descriptor and tables ready, and had its output
-    // stores acknowledged (just before its done store)
+    // took the job, after its acquire fence, with the descriptor in LDS, and
+    // with its output stores acknowledged (just before its done store)
     uint64_t trace[4];
 };
 // Grid-wide control words, after the slots in the same mapped allocation.

@@ -67,22 +67,6 @@ using detail::u32x4;
 constexpr int kQThreads = 1024;  // most threads per slot: a 16 KiB chunk in one pass
 constexpr int kQBatch = 16;
 
-__device__ __forceinline__ uint32_t gmul8(uint32_t a, uint32_t b) {  // GF(2^8), poly 0x11d
-    uint32_t p = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        p ^= (b & 1u) ? a : 0u;
-        b >>= 1;
-        a <<= 1;
-        a ^= (a & 0x100u) ? 0x11du : 0u;
-    }
-    return p;
-}
-
-__device__ __forceinline__ uint32_t pack4(uint32_t c, uint32_t a, uint32_t b, uint32_t d, uint32_t e) {
-    return gmul8(c, a) | gmul8(c, b) << 8 | gmul8(c, d) << 16 | gmul8(c, e) << 24;
-}
-
 __device__ __forceinline__ uint32_t tmul(const uint32_t *t, uint32_t x) {  // gf8_mul over LDS tables
     return __builtin_amdgcn_perm(t[1], t[0], x & 0x07070707u) ^ __builtin_amdgcn_perm(t[3], t[2], (x >> 3) & 0x07070707u) ^
            __builtin_amdgcn_perm(t[4], t[4], (x >> 6) & 0x03030303u);
@@ -132,7 +116,7 @@ __device__ __forceinline__ void code_unit(const uint64_t *addr, const uint32_t *
 #pragma unroll
             for (int r = 0; r < int(kQMaxDst); ++r) {
                 if (j0 + jj < ns && uint32_t(r) < nd) {
-                    const uint32_t *T = tab + (r * kQMaxSrc + j0 + jj) * 8;
+                    const uint32_t *T = tab + (r * ns + j0 + jj) * 8;
                     acc[r] ^= u32x4{tmul(T, x[jj].x), tmul(T, x[jj].y), tmul(T, x[jj].z), tmul(T, x[jj].w)};
                 }
             }
@@ -245,7 +229,12 @@ __device__ __forceinline__ void mark_active(uint64_t *act) {
     __hip_atomic_store(act, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-constexpr uint32_t kQDescWords = 8 + 2 * (kQMaxSrc + kQMaxDst) + kQMaxDst * kQMaxSrc / 4 + kQMaxSrc * kQBmRows / 4;
+// descriptor words read per job: hdr, src, dst, then the tables (byte-wise)
+// or the masks (bitmatrix); a job's own share is a prefix of that payload,
+// but the whole of it is read in the same round trip as the rest
+constexpr uint32_t kQHeadWords = 8 + 2 * (kQMaxSrc + kQMaxDst);
+constexpr uint32_t kQDescWords = kQHeadWords + kQMaxDst * kQMaxSrc * 8;
+constexpr uint32_t kQDescWordsBm = kQHeadWords + kQMaxSrc * kQBmRows / 4;
 
 // Workgroup b serves slot b / parts as part b % parts: part 0 polls the
 // slot in host memory and, when it takes a job, publishes its number in
@@ -258,24 +247,23 @@ constexpr uint32_t kQDescWords = 8 + 2 * (kQMaxSrc + kQMaxDst) + kQMaxDst * kQMa
 // is never taken, queue_try).
 __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t *ctl, uint64_t *act, uint64_t *link,
                                                          uint64_t epoch, uint64_t idle_ticks, uint32_t nthr,
-                                                         uint32_t nslots, uint32_t parts) {
-    __shared__ uint32_t desc[kQDescWords];  // the slot's descriptor: hdr, src, dst, coef_w, mask_w
-    __shared__ uint32_t tab[kQMaxDst * kQMaxSrc * 8];
+                                                         uint32_t nslots, uint32_t parts, uint32_t desc_words) {
+    __shared__ uint32_t desc[kQDescWords];  // the slot's descriptor: hdr, src, dst, tab_w | mask_w
     __shared__ uint32_t cmd;
     const uint32_t si = blockIdx.x / parts, part = blockIdx.x - si * parts;
     QSlot *s = slots + si;
     uint64_t *go = link + si, *left = link + nslots + si;
     const uint32_t t = threadIdx.x;
     const bool leader = blockIdx.x == 0;
-    uint64_t last = 0, t0 = 0, t_take = 0;
+    uint64_t last = 0, t0 = 0, t_take = 0, t_fence = 0;
     if (t == 0) {
         last = sys_load(&s->done[part]);
         t0 = __builtin_amdgcn_s_memrealtime();
     }
     const uint32_t *hdr = desc;
     const uint64_t *addr = reinterpret_cast<const uint64_t *>(desc + 8);
-    const uint32_t *cw = desc + 8 + 2 * (kQMaxSrc + kQMaxDst);
-    const uint8_t *mk = reinterpret_cast<const uint8_t *>(cw + kQMaxDst * kQMaxSrc / 4);
+    const uint32_t *tab = desc + kQHeadWords;
+    const uint8_t *mk = reinterpret_cast<const uint8_t *>(desc + kQHeadWords);
     for (;;) {
         if (t == 0 && part != 0) {  // the other parts: part 0's jobs, from device memory
             uint32_t c = 0;
@@ -316,6 +304,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                 if (q > last) {  // a withdrawn job moves seq back (queue_try)
                     t_take = __builtin_amdgcn_s_memrealtime();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once per job
+                    t_fence = __builtin_amdgcn_s_memrealtime();
                     last = q;
                     c = 1;
                     if (parts > 1) __hip_atomic_store(go, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -343,27 +332,15 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
         }
         __syncthreads();
         if (cmd == 0) return;  // uniform: stop or grid idle
-        {  // descriptor: hdr, src, dst as 32-bit words, coefficients, masks
+        {  // descriptor: hdr, src, dst as 32-bit words, then tables or masks
             const uint32_t *sw = reinterpret_cast<const uint32_t *>(&s->hdr[0]);
-            for (uint32_t i = t; i < kQDescWords; i += nthr) desc[i] = sys_load(sw + i);
+            for (uint32_t i = t; i < desc_words; i += nthr) desc[i] = sys_load(sw + i);
         }
         __syncthreads();
         const uint32_t ns = hdr[0], nd = hdr[1], bytes = hdr[2], acc_in = hdr[3], w = hdr[4], P = hdr[5];
         const bool traced = hdr[6] != 0u && part == 0 && t == 0;
-        uint64_t t_desc = 0;
-        if (w == 0) {  // byte-wise GF(2^8): v_perm tables from the coefficient bytes
-            for (uint32_t e = t; e < nd * ns; e += nthr) {  // nthr may be 64 (one-wave parts)
-                const uint32_t r = e / ns, j = e - r * ns, b = r * kQMaxSrc + j;
-                const uint32_t c = (cw[b / 4] >> (8 * (b % 4))) & 0xffu;
-                uint32_t *T = tab + b * 8;
-                T[0] = pack4(c, 0, 1, 2, 3);
-                T[1] = pack4(c, 4, 5, 6, 7);
-                T[2] = pack4(c, 0, 8, 16, 24);
-                T[3] = pack4(c, 32, 40, 48, 56);
-                T[4] = pack4(c, 0, 64, 128, 192);
-            }
-            __syncthreads();
-            if (traced) t_desc = __builtin_amdgcn_s_memrealtime();
+        const uint64_t t_desc = traced ? __builtin_amdgcn_s_memrealtime() : 0;
+        if (w == 0) {  // byte-wise GF(2^8): the host's v_perm tables, read in place from LDS
             // this part's units: passes of nthr units, part-th of every parts
             const uint32_t full = bytes / 16, me = part * nthr + t, step = parts * nthr;
             for (uint32_t u = me; u < full; u += step)
@@ -371,7 +348,6 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             if (bytes % 16 && me == full % step)  // the partial last unit
                 code_unit<false>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
         } else {
-            if (traced) t_desc = __builtin_amdgcn_s_memrealtime();
             const uint32_t me = part * nthr + t, step = parts * nthr;
             switch (w) {  // uniform
                 case 1: bm_job<1>(addr, mk, ns, nd, acc_in, P, me, step); break;
@@ -397,14 +373,25 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
         if (traced) {  // measurement only (mec_queue_trace_enable): vector stores before the release
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
             __hip_atomic_store(&s->trace[0], t_take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&s->trace[1], t_desc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&s->trace[2], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&s->trace[1], t_fence, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&s->trace[2], t_desc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&s->trace[3], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (t == 0) {
             __hip_atomic_store(&s->done[part], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             if (part == 0) mark_active(act + si);
         }
     }
+}
+
+// Gf8Coef of every GF(2^8) value, built once (gf8_coef: 20 field products)
+const Gf8Coef *gf8_coef_table() {
+    static const std::vector<Gf8Coef> t = [] {
+        std::vector<Gf8Coef> v(256);
+        for (int c = 0; c < 256; ++c) v[size_t(c)] = gf8_coef(uint8_t(c));
+        return v;
+    }();
+    return t.data();
 }
 
 uint64_t mono_ns() {  // CLOCK_MONOTONIC, the clock mec_queue_trace reports in
@@ -415,7 +402,7 @@ uint64_t mono_ns() {  // CLOCK_MONOTONIC, the clock mec_queue_trace reports in
 
 // The calling thread's last traced queue call (mec_queue_last_trace).
 struct QTrace {
-    uint64_t host_post_ns, host_seen_ns, dev_take, dev_desc, dev_end;
+    uint64_t host_post_ns, host_seen_ns, dev_take, dev_fence, dev_desc, dev_end;
     uint32_t parts, valid;
 };
 QTrace &last_trace() {
@@ -434,7 +421,8 @@ int queue_launch(mec_ctx *c, HostQueue *q) {
     __atomic_store_n(q->ctl_host + kQCtlExit, 0u, __ATOMIC_RELEASE);
     ++q->epoch;
     hipLaunchKernelGGL(queue_kernel, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev, q->ctl_dev,
-                       q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts);
+                       q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts,
+                       c->byte_wise() ? kQDescWords : kQDescWordsBm);
     HIP_TRY(hipGetLastError());
     q->launches++;
     return MEC_OK;
@@ -604,11 +592,8 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     s->hdr[6] = traced ? 1u : 0u;
     for (size_t j = 0; j < ns; ++j) s->src[j] = addrs[j];
     for (size_t r = 0; r < nd; ++r) s->dst[r] = addrs[ns + r];
-    if (c->byte_wise()) {
-        uint8_t cb[kQMaxDst * kQMaxSrc] = {};
-        for (size_t r = 0; r < nd; ++r)
-            for (size_t j = 0; j < ns; ++j) cb[r * kQMaxSrc + j] = coef[r * ns + j];
-        std::memcpy(s->coef_w, cb, sizeof(cb));
+    if (c->byte_wise()) {  // the v_perm tables, [output][source] (a table per GF(2^8) value)
+        for (size_t b = 0; b < nd * ns; ++b) std::memcpy(&s->tab_w[b * 8], &gf8_coef_table()[coef[b]], sizeof(Gf8Coef));
     } else {  // GF(2^w) coefficients -> bitmatrix rows (jerasure_matrix_to_bitmatrix)
         const Field &f = Field::get(int(c->w));
         uint8_t mk[kQMaxSrc][kQBmRows] = {};
@@ -678,8 +663,9 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
         tr.host_seen_ns = mono_ns();
         tr.host_post_ns = t_post;
         tr.dev_take = s->trace[0];
-        tr.dev_desc = s->trace[1];
-        tr.dev_end = s->trace[2];
+        tr.dev_fence = s->trace[1];
+        tr.dev_desc = s->trace[2];
+        tr.dev_end = s->trace[3];
         tr.parts = q->parts;
         tr.valid = 1;
     }
@@ -714,6 +700,7 @@ int mec_queue_last_trace(mec_queue_trace *out) {
     out->host_post_ns = t.host_post_ns;
     out->host_seen_ns = t.host_seen_ns;
     out->dev_take = t.dev_take;
+    out->dev_fence = t.dev_fence;
     out->dev_desc = t.dev_desc;
     out->dev_end = t.dev_end;
     out->parts = t.parts;

@@ -10,7 +10,8 @@
 // with mec_queue_trace_enable on.  Per call:
 //   pre       API entry -> job posted           (host)
 //   poll      posted -> part 0 took the job     (PCIe poll of the slot)
-//   desc      took -> descriptor + tables ready  (device: descriptor read over PCIe)
+//   fence     took -> its acquire fence done     (device)
+//   desc      fence -> descriptor + tables in LDS (device: one read over PCIe)
 //   code      tables -> output stores acked     (device: source loads, math, stores)
 //   complete  stores acked -> host saw done     (done release + host poll)
 //   post      done seen -> API return            (host)
@@ -41,6 +42,7 @@ __global__ void calib_kernel(const uint64_t *host_word, uint64_t *out, int n) {
     for (int i = 0; i < n; ++i) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         const uint64_t v = __hip_atomic_load(host_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the read has returned
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
         out[3 * i] = t0;
         out[3 * i + 1] = v;
@@ -131,7 +133,7 @@ int main(int argc, char **argv) {
     std::vector<const uint8_t *> data(k);
     std::vector<uint8_t *> par(m, nullptr);
     for (uint32_t j = 0; j < k; ++j) data[j] = slab + j * slot + 8;
-    std::vector<double> seg[7];
+    std::vector<double> seg[8];
     const int warm = std::min(2000, calls / 4 + 1);
     uint64_t t_start = 0;
     for (int it = 0; it < warm + calls; ++it) {
@@ -143,22 +145,24 @@ int main(int argc, char **argv) {
         mec_queue_trace tr;
         if (mec_queue_last_trace(&tr) != MEC_OK || it < warm) continue;  // launch path (no trace)
         const double take = double(tr.dev_take) * ns_per_tick - off;
+        const double fence = double(tr.dev_fence) * ns_per_tick - off;
         const double desc = double(tr.dev_desc) * ns_per_tick - off;
         const double end = double(tr.dev_end) * ns_per_tick - off;
         seg[0].push_back((double(tr.host_post_ns) - double(a)) * 1e-3);
         seg[1].push_back((take - double(tr.host_post_ns)) * 1e-3);
-        seg[2].push_back((desc - take) * 1e-3);
-        seg[3].push_back((end - desc) * 1e-3);
-        seg[4].push_back((double(tr.host_seen_ns) - end) * 1e-3);
-        seg[5].push_back((double(b) - double(tr.host_seen_ns)) * 1e-3);
-        seg[6].push_back(double(b - a) * 1e-3);
+        seg[2].push_back((fence - take) * 1e-3);
+        seg[3].push_back((desc - fence) * 1e-3);
+        seg[4].push_back((end - desc) * 1e-3);
+        seg[5].push_back((double(tr.host_seen_ns) - end) * 1e-3);
+        seg[6].push_back((double(b) - double(tr.host_seen_ns)) * 1e-3);
+        seg[7].push_back(double(b - a) * 1e-3);
     }
     const double dt = double(mono_ns() - t_start) * 1e-9;
-    const char *names[7] = {"pre", "poll", "desc", "code", "complete", "post", "total"};
+    const char *names[8] = {"pre", "poll", "fence", "desc", "code", "complete", "post", "total"};
     printf("{\"bench\": \"queue_latency\", \"family\": \"%s\", \"k\": %u, \"m\": %u, \"chunk\": %u, \"outputs\": %u, "
            "\"registered\": %d, \"calls\": %d, \"traced\": %zu, \"calls_per_s\": %.1f, \"clock_window_us\": %.3f",
-           argv[1], k, m, cs, nd, reg ? 1 : 0, calls, seg[6].size(), calls / dt, window * 1e-3);
-    for (int i = 0; i < 7; ++i)
+           argv[1], k, m, cs, nd, reg ? 1 : 0, calls, seg[7].size(), calls / dt, window * 1e-3);
+    for (int i = 0; i < 8; ++i)
         printf(", \"%s_us\": [%.3f, %.3f]", names[i], pct(seg[i], 0.5), pct(seg[i], 0.9));
     printf("}\n");
     if (reg) mec_host_unregister(slab);
