@@ -152,7 +152,6 @@ struct HostQueue {
     uint64_t idle_ticks = 0, timeout_ms = 5000;
     std::atomic<bool> *busy = nullptr;
     std::atomic<bool> trace{false};   // mec_queue_trace_enable
-    bool sysio = true;                // queue_kernel<true>: system-scope chunk access, no per-job fences
     hipStream_t stream = nullptr;
     std::mutex mu;  // launches
     std::atomic<uint64_t> calls{0}, launches{0};

@@ -88,77 +88,28 @@ __device__ __forceinline__ void st_part(uint8_t *p, const u32x4 &v, uint32_t n) 
         if (uint32_t(i) < n) p[i] = uint8_t(w[i / 4] >> (8 * (i % 4)));
 }
 
-// System-scope chunk access (SYS kernels, MEC_QUEUE_SYSIO): every load and
-// store of a caller's chunk carries sc0 sc1, so it bypasses the GPU's caches
-// both ways — no line of an earlier job can be read, and an output is in
-// host memory once its store is acknowledged.  That is what lets a SYS job
-// run without the system-scope acquire at take and the release before its
-// done word (each a full L2 invalidate / write-back, ~1.7 us,
-// MI355X_MICROARCH.md).  Full units through buffer instructions (the chunk
-// base uniform, a 32-bit lane offset), tails byte by byte through atomics.
-constexpr int kAuxSys = 1 | 16;  // sc0 | sc1: system scope
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t sys_rsrc(uint64_t base) {
-    return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(base), 0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ u32x4 sys_ld16(uint64_t base, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b128(sys_rsrc(base), off, 0, kAuxSys);
-}
-__device__ __forceinline__ void sys_st16(uint64_t base, uint32_t off, u32x4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(v, sys_rsrc(base), off, 0, kAuxSys);
-}
-__device__ __forceinline__ u32x2 sys_ld8(uint64_t base, uint32_t off) {
-    return __builtin_amdgcn_raw_buffer_load_b64(sys_rsrc(base), off, 0, kAuxSys);
-}
-__device__ __forceinline__ void sys_st8(uint64_t base, uint32_t off, u32x2 v) {
-    __builtin_amdgcn_raw_buffer_store_b64(v, sys_rsrc(base), off, 0, kAuxSys);
-}
-__device__ __forceinline__ uint8_t sys_ldb(const uint8_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void sys_stb(uint8_t *p, uint8_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-template <bool SYS>
-__device__ __forceinline__ u32x4 ld_part_s(const uint8_t *p, uint32_t n) {
-    if constexpr (!SYS) return ld_part(p, n);
-    uint32_t w[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if (uint32_t(i) < n) w[i / 4] |= uint32_t(sys_ldb(p + i)) << (8 * (i % 4));
-    return u32x4{w[0], w[1], w[2], w[3]};
-}
-template <bool SYS>
-__device__ __forceinline__ void st_part_s(uint8_t *p, const u32x4 &v, uint32_t n) {
-    if constexpr (!SYS) return st_part(p, v, n);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 16; ++i)
-        if (uint32_t(i) < n) sys_stb(p + i, uint8_t(w[i / 4] >> (8 * (i % 4))));
-}
-
 // One 16-byte unit (FULL) or the n-byte tail at byte offset off of every
 // chunk: acc[r] (^)= sum_j coef[r][j] * src_j.  Source loads are issued in
 // groups of kQBatch back to back, one PCIe round trip per group.
-template <bool FULL, bool SYS>
+template <bool FULL>
 __device__ __forceinline__ void code_unit(const uint64_t *addr, const uint32_t *tab, uint32_t ns, uint32_t nd,
                                           uint32_t acc_in, uint64_t off, uint32_t n) {
-    auto ld = [&](uint64_t a) {  // chunk base a, this unit at off
-        if constexpr (FULL && SYS) return sys_ld16(a, uint32_t(off));
-        else if constexpr (FULL) return *reinterpret_cast<const u32x4 *>(a + off);
-        else return ld_part_s<SYS>(reinterpret_cast<const uint8_t *>(a + off), n);
+    auto ld = [&](uint64_t p) {
+        if constexpr (FULL) return *reinterpret_cast<const u32x4 *>(p);
+        else return ld_part(reinterpret_cast<const uint8_t *>(p), n);
     };
     u32x4 acc[kQMaxDst];
 #pragma unroll
     for (int r = 0; r < int(kQMaxDst); ++r) {
         const uint64_t d = addr[kQMaxSrc + r];
-        acc[r] = (acc_in && uint32_t(r) < nd && d) ? ld(d) : u32x4{0, 0, 0, 0};
+        acc[r] = (acc_in && uint32_t(r) < nd && d) ? ld(d + off) : u32x4{0, 0, 0, 0};
     }
     for (uint32_t j0 = 0; j0 < ns; j0 += kQBatch) {
         u32x4 x[kQBatch];
 #pragma unroll
         for (int jj = 0; jj < kQBatch; ++jj) {
             const uint64_t a = j0 + jj < ns ? addr[j0 + jj] : 0;  // 0: Coding::zeros / past ns
-            x[jj] = a ? ld(a) : u32x4{0, 0, 0, 0};
+            x[jj] = a ? ld(a + off) : u32x4{0, 0, 0, 0};
         }
 #pragma unroll
         for (int jj = 0; jj < kQBatch; ++jj) {
@@ -175,9 +126,8 @@ __device__ __forceinline__ void code_unit(const uint64_t *addr, const uint32_t *
     for (int r = 0; r < int(kQMaxDst); ++r) {
         const uint64_t d = addr[kQMaxSrc + r];
         if (uint32_t(r) >= nd || !d) continue;
-        if constexpr (FULL && SYS) sys_st16(d, uint32_t(off), acc[r]);
-        else if constexpr (FULL) *reinterpret_cast<u32x4 *>(d + off) = acc[r];
-        else st_part_s<SYS>(reinterpret_cast<uint8_t *>(d + off), acc[r], n);
+        if constexpr (FULL) *reinterpret_cast<u32x4 *>(d + off) = acc[r];
+        else st_part(reinterpret_cast<uint8_t *>(d + off), acc[r], n);
     }
 }
 
@@ -188,44 +138,33 @@ __device__ __forceinline__ u32x2 bm_axor(u32x2 d, uint32_t m, u32x2 acc) {
                  uint32_t(__builtin_amdgcn_bitop3_b32(d.y, m, acc.y, 0x6A))};
 }
 
-// 8 bytes (or the n < 8 tail) at base + off
-template <bool SYS>
-__device__ __forceinline__ u32x2 ld8(uint64_t base, uint64_t off, uint32_t n) {
-    if (n == 8) {
-        if constexpr (SYS) return sys_ld8(base, uint32_t(off));
-        else return *reinterpret_cast<const u32x2 *>(base + off);
-    }
-    const uint8_t *b = reinterpret_cast<const uint8_t *>(base + off);
+__device__ __forceinline__ u32x2 ld8(uint64_t p, uint32_t n) {
+    if (n == 8) return *reinterpret_cast<const u32x2 *>(p);
+    const uint8_t *b = reinterpret_cast<const uint8_t *>(p);
     uint32_t w[2] = {0, 0};
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-        if (uint32_t(i) < n) w[i / 4] |= uint32_t(SYS ? sys_ldb(b + i) : b[i]) << (8 * (i % 4));
+        if (uint32_t(i) < n) w[i / 4] |= uint32_t(b[i]) << (8 * (i % 4));
     return u32x2{w[0], w[1]};
 }
 
-template <bool SYS>
-__device__ __forceinline__ void st8(uint64_t base, uint64_t off, u32x2 v, uint32_t n) {
+__device__ __forceinline__ void st8(uint64_t p, u32x2 v, uint32_t n) {
     if (n == 8) {
-        if constexpr (SYS) sys_st8(base, uint32_t(off), v);
-        else *reinterpret_cast<u32x2 *>(base + off) = v;
+        *reinterpret_cast<u32x2 *>(p) = v;
         return;
     }
-    uint8_t *b = reinterpret_cast<uint8_t *>(base + off);
+    uint8_t *b = reinterpret_cast<uint8_t *>(p);
     const uint32_t w[2] = {v.x, v.y};
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        if (uint32_t(i) >= n) continue;
-        const uint8_t x = uint8_t(w[i / 4] >> (8 * (i % 4)));
-        if constexpr (SYS) sys_stb(b + i, x);
-        else b[i] = x;
-    }
+    for (int i = 0; i < 8; ++i)
+        if (uint32_t(i) < n) b[i] = uint8_t(w[i / 4] >> (8 * (i % 4)));
 }
 
 // The n-byte slice (n <= 8) at offset off of every packet: output packet
 // (r, l) (^)= XOR over (j, x) with bit x of mk[j][r*W + l] of source packet
 // (j, x) (jerasure_do_scheduled_operations' result, jerasure.c:1162-1185).
 // Sources are loaded B at a time (B*W slices in flight, one PCIe round trip).
-template <int W, bool SYS>
+template <int W>
 __device__ __forceinline__ void bm_unit(const uint64_t *addr, const uint8_t *mk, uint32_t ns, uint32_t nd,
                                         uint32_t acc_in, uint64_t off, uint32_t n, uint64_t P) {
     constexpr int B = W >= 16 ? 1 : 16 / W;
@@ -235,7 +174,7 @@ __device__ __forceinline__ void bm_unit(const uint64_t *addr, const uint8_t *mk,
         const uint64_t d = addr[kQMaxSrc + r];
 #pragma unroll
         for (int l = 0; l < W; ++l)
-            acc[r * W + l] = (acc_in && uint32_t(r) < nd && d) ? ld8<SYS>(d, l * P + off, n) : u32x2{0, 0};
+            acc[r * W + l] = (acc_in && uint32_t(r) < nd && d) ? ld8(d + l * P + off, n) : u32x2{0, 0};
     }
     for (uint32_t j0 = 0; j0 < ns; j0 += B) {
         u32x2 x[B][W];
@@ -243,7 +182,7 @@ __device__ __forceinline__ void bm_unit(const uint64_t *addr, const uint8_t *mk,
         for (int jj = 0; jj < B; ++jj) {
             const uint64_t a = j0 + jj < ns ? addr[j0 + jj] : 0;  // 0: Coding::zeros / past ns
 #pragma unroll
-            for (int xw = 0; xw < W; ++xw) x[jj][xw] = a ? ld8<SYS>(a, xw * P + off, n) : u32x2{0, 0};
+            for (int xw = 0; xw < W; ++xw) x[jj][xw] = a ? ld8(a + xw * P + off, n) : u32x2{0, 0};
         }
 #pragma unroll
         for (int jj = 0; jj < B; ++jj) {
@@ -267,17 +206,17 @@ __device__ __forceinline__ void bm_unit(const uint64_t *addr, const uint8_t *mk,
         const uint64_t d = addr[kQMaxSrc + r];
         if (uint32_t(r) >= nd || !d) continue;
 #pragma unroll
-        for (int l = 0; l < W; ++l) st8<SYS>(d, l * P + off, acc[r * W + l], n);
+        for (int l = 0; l < W; ++l) st8(d + l * P + off, acc[r * W + l], n);
     }
 }
 
-template <int W, bool SYS>
+template <int W>
 __device__ __forceinline__ void bm_job(const uint64_t *addr, const uint8_t *mk, uint32_t ns, uint32_t nd,
                                        uint32_t acc_in, uint32_t P, uint32_t t, uint32_t nthr) {
     const uint32_t units = (P + 7) / 8;
     for (uint32_t u = t; u < units; u += nthr) {
         const uint32_t off = u * 8;
-        bm_unit<W, SYS>(addr, mk, ns, nd, acc_in, off, P - off < 8 ? P - off : 8, P);
+        bm_unit<W>(addr, mk, ns, nd, acc_in, off, P - off < 8 ? P - off : 8, P);
     }
 }
 
@@ -306,7 +245,6 @@ constexpr uint32_t kQDescWordsBm = kQHeadWords + kQMaxSrc * kQBmRows / 4;
 // the other parts leave only after that, having run every job part 0 took
 // — so a job is run by all of a slot's parts or by none (a withdrawn job
 // is never taken, queue_try).
-template <bool SYS>
 __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t *ctl, uint64_t *act, uint64_t *link,
                                                          uint64_t epoch, uint64_t idle_ticks, uint32_t nthr,
                                                          uint32_t nslots, uint32_t parts, uint32_t desc_words) {
@@ -337,9 +275,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                 const uint64_t lf = __hip_atomic_load(left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t q = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (q > last) {
-                    // SYS: this part reads the descriptor and chunks with
-                    // system-scope loads, nothing of the job through a cache
-                    if constexpr (!SYS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                     last = q;
                     c = 1;
                     break;
@@ -352,7 +288,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     const uint64_t q2 = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (q2 > last) {
-                        if constexpr (!SYS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
                         last = q2;
                         c = 1;
                     }
@@ -367,16 +303,11 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                 const uint64_t q = __hip_atomic_load(&s->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if (q > last) {  // a withdrawn job moves seq back (queue_try)
                     t_take = __builtin_amdgcn_s_memrealtime();
-                    // system scope, once per job; SYS jobs read everything
-                    // with system-scope loads (no cached line to drop)
-                    if constexpr (!SYS) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once per job
                     t_fence = __builtin_amdgcn_s_memrealtime();
                     last = q;
                     c = 1;
-                    if (parts > 1) {  // SYS: the other parts read nothing part 0 wrote
-                        if constexpr (SYS) __hip_atomic_store(go, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        else __hip_atomic_store(go, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    }
+                    if (parts > 1) __hip_atomic_store(go, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                     break;
                 }
                 if (n % 64 == 0) {
@@ -413,20 +344,20 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             // this part's units: passes of nthr units, part-th of every parts
             const uint32_t full = bytes / 16, me = part * nthr + t, step = parts * nthr;
             for (uint32_t u = me; u < full; u += step)
-                code_unit<true, SYS>(addr, tab, ns, nd, acc_in, uint64_t(u) * 16, 16);
+                code_unit<true>(addr, tab, ns, nd, acc_in, uint64_t(u) * 16, 16);
             if (bytes % 16 && me == full % step)  // the partial last unit
-                code_unit<false, SYS>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
+                code_unit<false>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
         } else {
             const uint32_t me = part * nthr + t, step = parts * nthr;
             switch (w) {  // uniform
-                case 1: bm_job<1, SYS>(addr, mk, ns, nd, acc_in, P, me, step); break;
-                case 2: bm_job<2, SYS>(addr, mk, ns, nd, acc_in, P, me, step); break;
-                case 3: bm_job<3, SYS>(addr, mk, ns, nd, acc_in, P, me, step); break;
-                case 4: bm_job<4, SYS>(addr, mk, ns, nd, acc_in, P, me, step); break;
-                case 5: bm_job<5, SYS>(addr, mk, ns, nd, acc_in, P, me, step); break;
-                case 6: bm_job<6, SYS>(addr, mk, ns, nd, acc_in, P, me, step); break;
-                case 7: bm_job<7, SYS>(addr, mk, ns, nd, acc_in, P, me, step); break;
-                case 8: bm_job<8, SYS>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 1: bm_job<1>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 2: bm_job<2>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 3: bm_job<3>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 4: bm_job<4>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 5: bm_job<5>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 6: bm_job<6>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 7: bm_job<7>(addr, mk, ns, nd, acc_in, P, me, step); break;
+                case 8: bm_job<8>(addr, mk, ns, nd, acc_in, P, me, step); break;
                 default: break;
             }
         }
@@ -447,11 +378,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             __hip_atomic_store(&s->trace[3], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (t == 0) {
-            // SYS: every output store was write-through and has been
-            // acknowledged (the wait + barrier above), so a relaxed
-            // system-scope store orders after them without an L2 write-back
-            if constexpr (SYS) __hip_atomic_store(&s->done[part], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            else __hip_atomic_store(&s->done[part], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&s->done[part], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             if (part == 0) mark_active(act + si);
         }
     }
@@ -493,13 +420,9 @@ int queue_launch(mec_ctx *c, HostQueue *q) {
     DeviceGuard dg(c->device);
     __atomic_store_n(q->ctl_host + kQCtlExit, 0u, __ATOMIC_RELEASE);
     ++q->epoch;
-    const uint32_t dw = c->byte_wise() ? kQDescWords : kQDescWordsBm;
-    if (q->sysio)
-        hipLaunchKernelGGL(queue_kernel<true>, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev,
-                           q->ctl_dev, q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts, dw);
-    else
-        hipLaunchKernelGGL(queue_kernel<false>, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev,
-                           q->ctl_dev, q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts, dw);
+    hipLaunchKernelGGL(queue_kernel, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev, q->ctl_dev,
+                       q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts,
+                       c->byte_wise() ? kQDescWords : kQDescWordsBm);
     HIP_TRY(hipGetLastError());
     q->launches++;
     return MEC_OK;
@@ -565,9 +488,6 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     q->solo_max = uint32_t(env_u64("MEC_QUEUE_SOLO_MAX", q->max_chunk));
     q->idle_ticks = env_u64("MEC_QUEUE_IDLE_MS", 50) * 100000ull;  // s_memrealtime: 100 MHz
     q->timeout_ms = env_u64("MEC_QUEUE_TIMEOUT_MS", 5000);
-    // system-scope chunk access instead of the per-job acquire / release
-    // fences (queue_kernel<true>); MEC_QUEUE_SYSIO=0 keeps the fences
-    q->sysio = env_u64("MEC_QUEUE_SYSIO", 1) != 0;
     // workgroups per slot: one per MEC_QUEUE_PART_THREADS units (default
     // kQThreads: a 16 KiB pass of 16-byte units), at most kQMaxParts;
     // MEC_QUEUE_PARTS sets the count directly (A/Bs)
@@ -585,7 +505,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     // launches beside it (calls beyond the slots, batches) keep CUs to run on
     {
         int per_cu = 0, cus = 0;
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_kernel<false>, int(q->threads), 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_kernel, int(q->threads), 0));
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         const uint32_t cap = uint32_t(std::max(1, per_cu * cus / 2)) / q->parts;
         slots = std::max<uint32_t>(1, std::min(slots, cap));
