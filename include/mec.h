@@ -333,6 +333,7 @@ typedef struct {
     uint64_t dev_take;      /* device ticks: job taken (seq seen) */
     uint64_t dev_fence;     /* its system-scope acquire fence done */
     uint64_t dev_desc;      /* descriptor (incl. coefficient tables) in LDS */
+    uint64_t dev_loaded;    /* thread 0's first source loads returned (byte-wise jobs; 0 otherwise) */
     uint64_t dev_end;       /* output stores acknowledged, before the done store */
     uint32_t parts, pad;
 } mec_queue_trace;

@@ -113,7 +113,9 @@ constexpr uint32_t kQMaxParts = 64;  // workgroups per slot (one call's chunk sp
 constexpr uint64_t kQDrainFactor = 4;
 constexpr uint32_t kQBmRows = kQMaxDst * 8;  // bitmatrix output packet rows (outputs x w <= 8)
 struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
-    uint64_t seq;            // host -> GPU: number of the posted job
+    // host -> GPU: (number of the posted job << 16) | (sources << 8) |
+    // outputs — the poll that sees a job also sizes its descriptor read
+    uint64_t seq;
     uint64_t pad0[15];
     uint64_t done[kQMaxParts];  // GPU -> host: number of the last job each part finished
     // sources, outputs, chunk bytes, accumulate, w (0: byte-wise GF(2^8);
@@ -123,15 +125,16 @@ struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
     uint64_t dst[kQMaxDst];  // (0 = unwanted output)
     union {
         // byte-wise: the v_perm tables of coefficient (output r, source j)
-        // at (r * sources + j) * 8 dwords (t0 t1 u0 u1 v, gf8_kernel.hpp),
+        // at (r * sources + j) * 5 dwords (t0 t1 u0 u1 v, gf8_kernel.hpp),
         // built on the host (a table per GF(2^8) value, computed once)
-        uint32_t tab_w[kQMaxDst * kQMaxSrc * 8];
+        uint32_t tab_w[kQMaxDst * kQMaxSrc * 5];
         uint32_t mask_w[kQMaxSrc * kQBmRows / 4];  // bitmatrix bytes [source][output*w + l], bit x
     };
     // GPU -> host when hdr[6] (trace) is set: part 0's s_memrealtime when it
-    // took the job, after its acquire fence, with the descriptor in LDS, and
-    // with its output stores acknowledged (just before its done store)
-    uint64_t trace[4];
+    // took the job, after its acquire fence, with the descriptor in LDS,
+    // when thread 0's source loads had returned, and with its output stores
+    // acknowledged (just before its done store)
+    uint64_t trace[5];
 };
 // Grid-wide control words, after the slots in the same mapped allocation.
 enum : uint32_t { kQCtlStop = 0, kQCtlExit = 1, kQCtlWords = 2 };

@@ -93,7 +93,7 @@ __device__ __forceinline__ void st_part(uint8_t *p, const u32x4 &v, uint32_t n) 
 // groups of kQBatch back to back, one PCIe round trip per group.
 template <bool FULL>
 __device__ __forceinline__ void code_unit(const uint64_t *addr, const uint32_t *tab, uint32_t ns, uint32_t nd,
-                                          uint32_t acc_in, uint64_t off, uint32_t n) {
+                                          uint32_t acc_in, uint64_t off, uint32_t n, uint64_t *t_loaded = nullptr) {
     auto ld = [&](uint64_t p) {
         if constexpr (FULL) return *reinterpret_cast<const u32x4 *>(p);
         else return ld_part(reinterpret_cast<const uint8_t *>(p), n);
@@ -111,12 +111,16 @@ __device__ __forceinline__ void code_unit(const uint64_t *addr, const uint32_t *
             const uint64_t a = j0 + jj < ns ? addr[j0 + jj] : 0;  // 0: Coding::zeros / past ns
             x[jj] = a ? ld(a + off) : u32x4{0, 0, 0, 0};
         }
+        if (t_loaded && j0 == 0) {  // traced jobs, thread 0 only: when its first loads returned
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            *t_loaded = __builtin_amdgcn_s_memrealtime();
+        }
 #pragma unroll
         for (int jj = 0; jj < kQBatch; ++jj) {
 #pragma unroll
             for (int r = 0; r < int(kQMaxDst); ++r) {
                 if (j0 + jj < ns && uint32_t(r) < nd) {
-                    const uint32_t *T = tab + (r * ns + j0 + jj) * 8;
+                    const uint32_t *T = tab + (r * ns + j0 + jj) * 5;
                     acc[r] ^= u32x4{tmul(T, x[jj].x), tmul(T, x[jj].y), tmul(T, x[jj].z), tmul(T, x[jj].w)};
                 }
             }
@@ -233,8 +237,13 @@ __device__ __forceinline__ void mark_active(uint64_t *act) {
 // or the masks (bitmatrix); a job's own share is a prefix of that payload,
 // but the whole of it is read in the same round trip as the rest
 constexpr uint32_t kQHeadWords = 8 + 2 * (kQMaxSrc + kQMaxDst);
-constexpr uint32_t kQDescWords = kQHeadWords + kQMaxDst * kQMaxSrc * 8;
-constexpr uint32_t kQDescWordsBm = kQHeadWords + kQMaxSrc * kQBmRows / 4;
+constexpr uint32_t kQDescWords = kQHeadWords + kQMaxSrc * kQBmRows / 4;  // >= the tables' kQMaxDst * kQMaxSrc * 5
+static_assert(kQMaxSrc * kQBmRows / 4 >= kQMaxDst * kQMaxSrc * 5, "descriptor LDS holds the tables");
+static_assert(kQHeadWords % 4 == 0, "16-byte descriptor loads");
+// dwords of a job's descriptor: the head, then its tables / masks
+__device__ __forceinline__ uint32_t desc_words(uint32_t ns, uint32_t nd, bool bitmatrix) {
+    return kQHeadWords + (bitmatrix ? ns * (kQBmRows / 4) : nd * ns * 5);
+}
 
 // Workgroup b serves slot b / parts as part b % parts: part 0 polls the
 // slot in host memory and, when it takes a job, publishes its number in
@@ -247,15 +256,16 @@ constexpr uint32_t kQDescWordsBm = kQHeadWords + kQMaxSrc * kQBmRows / 4;
 // is never taken, queue_try).
 __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t *ctl, uint64_t *act, uint64_t *link,
                                                          uint64_t epoch, uint64_t idle_ticks, uint32_t nthr,
-                                                         uint32_t nslots, uint32_t parts, uint32_t desc_words) {
-    __shared__ uint32_t desc[kQDescWords];  // the slot's descriptor: hdr, src, dst, tab_w | mask_w
-    __shared__ uint32_t cmd;
+                                                         uint32_t nslots, uint32_t parts, uint32_t bitmatrix) {
+    __shared__ u32x4 desc4[kQDescWords / 4];  // the slot's descriptor: hdr, src, dst, tab_w | mask_w
+    __shared__ uint32_t cmd, shape;
+    uint32_t *desc = reinterpret_cast<uint32_t *>(desc4);
     const uint32_t si = blockIdx.x / parts, part = blockIdx.x - si * parts;
     QSlot *s = slots + si;
     uint64_t *go = link + si, *left = link + nslots + si;
     const uint32_t t = threadIdx.x;
     const bool leader = blockIdx.x == 0;
-    uint64_t last = 0, t0 = 0, t_take = 0, t_fence = 0;
+    uint64_t last = 0, t0 = 0, t_take = 0, t_fence = 0, t_loaded = 0;
     if (t == 0) {
         last = sys_load(&s->done[part]);
         t0 = __builtin_amdgcn_s_memrealtime();
@@ -274,9 +284,10 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             for (;;) {
                 const uint64_t lf = __hip_atomic_load(left, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t q = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (q > last) {
+                if ((q >> 16) > last) {  // go = part 0's seq word (job number, shape)
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                    last = q;
+                    last = q >> 16;
+                    shape = uint32_t(q & 0xffffu);
                     c = 1;
                     break;
                 }
@@ -287,9 +298,10 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
                     // seen with the new `left` would skip part 0's last job
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                     const uint64_t q2 = __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (q2 > last) {
+                    if ((q2 >> 16) > last) {
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                        last = q2;
+                        last = q2 >> 16;
+                        shape = uint32_t(q2 & 0xffffu);
                         c = 1;
                     }
                     break;
@@ -301,11 +313,12 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             uint32_t c = 0;
             for (uint32_t n = 1;; ++n) {  // one PCIe read per poll; control words every 64th
                 const uint64_t q = __hip_atomic_load(&s->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                if (q > last) {  // a withdrawn job moves seq back (queue_try)
+                if ((q >> 16) > last) {  // a withdrawn job moves seq back (queue_try)
                     t_take = __builtin_amdgcn_s_memrealtime();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once per job
                     t_fence = __builtin_amdgcn_s_memrealtime();
-                    last = q;
+                    last = q >> 16;
+                    shape = uint32_t(q & 0xffffu);
                     c = 1;
                     if (parts > 1) __hip_atomic_store(go, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
                     break;
@@ -332,9 +345,11 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
         }
         __syncthreads();
         if (cmd == 0) return;  // uniform: stop or grid idle
-        {  // descriptor: hdr, src, dst as 32-bit words, then tables or masks
-            const uint32_t *sw = reinterpret_cast<const uint32_t *>(&s->hdr[0]);
-            for (uint32_t i = t; i < desc_words; i += nthr) desc[i] = sys_load(sw + i);
+        {  // descriptor: the head, then this job's tables or masks only (its
+           // size came with the seq word), 16 bytes per lane, one round trip
+            const uint32_t n4 = (desc_words(shape >> 8, shape & 0xffu, bitmatrix != 0) + 3) / 4;
+            const u32x4 *sw = reinterpret_cast<const u32x4 *>(&s->hdr[0]);
+            for (uint32_t i = t; i < n4; i += nthr) desc4[i] = __builtin_nontemporal_load(sw + i);
         }
         __syncthreads();
         const uint32_t ns = hdr[0], nd = hdr[1], bytes = hdr[2], acc_in = hdr[3], w = hdr[4], P = hdr[5];
@@ -344,7 +359,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             // this part's units: passes of nthr units, part-th of every parts
             const uint32_t full = bytes / 16, me = part * nthr + t, step = parts * nthr;
             for (uint32_t u = me; u < full; u += step)
-                code_unit<true>(addr, tab, ns, nd, acc_in, uint64_t(u) * 16, 16);
+                code_unit<true>(addr, tab, ns, nd, acc_in, uint64_t(u) * 16, 16, traced && u == me ? &t_loaded : nullptr);
             if (bytes % 16 && me == full % step)  // the partial last unit
                 code_unit<false>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
         } else {
@@ -375,7 +390,8 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             __hip_atomic_store(&s->trace[0], t_take, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&s->trace[1], t_fence, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&s->trace[2], t_desc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&s->trace[3], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&s->trace[3], t_loaded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&s->trace[4], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (t == 0) {
             __hip_atomic_store(&s->done[part], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -402,7 +418,7 @@ uint64_t mono_ns() {  // CLOCK_MONOTONIC, the clock mec_queue_trace reports in
 
 // The calling thread's last traced queue call (mec_queue_last_trace).
 struct QTrace {
-    uint64_t host_post_ns, host_seen_ns, dev_take, dev_fence, dev_desc, dev_end;
+    uint64_t host_post_ns, host_seen_ns, dev_take, dev_fence, dev_desc, dev_loaded, dev_end;
     uint32_t parts, valid;
 };
 QTrace &last_trace() {
@@ -422,7 +438,7 @@ int queue_launch(mec_ctx *c, HostQueue *q) {
     ++q->epoch;
     hipLaunchKernelGGL(queue_kernel, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev, q->ctl_dev,
                        q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts,
-                       c->byte_wise() ? kQDescWords : kQDescWordsBm);
+                       c->byte_wise() ? 0u : 1u);
     HIP_TRY(hipGetLastError());
     q->launches++;
     return MEC_OK;
@@ -593,7 +609,7 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     for (size_t j = 0; j < ns; ++j) s->src[j] = addrs[j];
     for (size_t r = 0; r < nd; ++r) s->dst[r] = addrs[ns + r];
     if (c->byte_wise()) {  // the v_perm tables, [output][source] (a table per GF(2^8) value)
-        for (size_t b = 0; b < nd * ns; ++b) std::memcpy(&s->tab_w[b * 8], &gf8_coef_table()[coef[b]], sizeof(Gf8Coef));
+        for (size_t b = 0; b < nd * ns; ++b) std::memcpy(&s->tab_w[b * 5], &gf8_coef_table()[coef[b]], sizeof(Gf8Coef));
     } else {  // GF(2^w) coefficients -> bitmatrix rows (jerasure_matrix_to_bitmatrix)
         const Field &f = Field::get(int(c->w));
         uint8_t mk[kQMaxSrc][kQBmRows] = {};
@@ -601,9 +617,10 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
             for (size_t j = 0; j < ns; ++j) bit_block(f, coef[r * ns + j], c->w, &mk[j][r * c->w], 1);
         std::memcpy(s->mask_w, mk, sizeof(mk));
     }
-    const uint64_t seq = __atomic_load_n(&s->seq, __ATOMIC_RELAXED) + 1;
+    const uint64_t seq = (__atomic_load_n(&s->seq, __ATOMIC_RELAXED) >> 16) + 1;
     const uint64_t t_post = traced ? mono_ns() : 0;
-    __atomic_store_n(&s->seq, seq, __ATOMIC_RELEASE);  // publishes the descriptor
+    // publishes the descriptor; the word carries its shape (sources, outputs)
+    __atomic_store_n(&s->seq, seq << 16 | uint64_t(ns) << 8 | uint64_t(nd), __ATOMIC_RELEASE);
     // wait for the workgroup; relaunch the grid if it idled out meanwhile
     rc = MEC_OK;
     bool taken = true;
@@ -630,7 +647,7 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
                 // may still be written; an accumulate job must not be run
                 // again on top of the parts that applied it).
                 if (dt > std::chrono::milliseconds(q->timeout_ms)) q->timeouts++;
-                __atomic_store_n(&s->seq, seq - 1, __ATOMIC_SEQ_CST);
+                __atomic_store_n(&s->seq, (seq - 1) << 16, __ATOMIC_SEQ_CST);
                 q->broken.store(true);
                 __atomic_store_n(q->ctl_host + kQCtlStop, 1u, __ATOMIC_RELEASE);
                 const Drain dr = queue_drained(
@@ -665,7 +682,8 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
         tr.dev_take = s->trace[0];
         tr.dev_fence = s->trace[1];
         tr.dev_desc = s->trace[2];
-        tr.dev_end = s->trace[3];
+        tr.dev_loaded = s->trace[3];
+        tr.dev_end = s->trace[4];
         tr.parts = q->parts;
         tr.valid = 1;
     }
@@ -702,6 +720,7 @@ int mec_queue_last_trace(mec_queue_trace *out) {
     out->dev_take = t.dev_take;
     out->dev_fence = t.dev_fence;
     out->dev_desc = t.dev_desc;
+    out->dev_loaded = t.dev_loaded;
     out->dev_end = t.dev_end;
     out->parts = t.parts;
     t.valid = 0;

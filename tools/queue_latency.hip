@@ -12,7 +12,8 @@
 //   poll      posted -> part 0 took the job     (PCIe poll of the slot)
 //   fence     took -> its acquire fence done     (device)
 //   desc      fence -> descriptor + tables in LDS (device: one read over PCIe)
-//   code      tables -> output stores acked     (device: source loads, math, stores)
+//   load      tables -> thread 0's source loads returned (device: one read over PCIe)
+//   code      loads returned -> output stores acked (device: math, stores, their acks)
 //   complete  stores acked -> host saw done     (done release + host poll)
 //   post      done seen -> API return            (host)
 // Device and host clocks are related by a calibration kernel that reads a
@@ -133,7 +134,7 @@ int main(int argc, char **argv) {
     std::vector<const uint8_t *> data(k);
     std::vector<uint8_t *> par(m, nullptr);
     for (uint32_t j = 0; j < k; ++j) data[j] = slab + j * slot + 8;
-    std::vector<double> seg[8];
+    std::vector<double> seg[9];
     const int warm = std::min(2000, calls / 4 + 1);
     uint64_t t_start = 0;
     for (int it = 0; it < warm + calls; ++it) {
@@ -147,22 +148,24 @@ int main(int argc, char **argv) {
         const double take = double(tr.dev_take) * ns_per_tick - off;
         const double fence = double(tr.dev_fence) * ns_per_tick - off;
         const double desc = double(tr.dev_desc) * ns_per_tick - off;
+        const double loaded = tr.dev_loaded ? double(tr.dev_loaded) * ns_per_tick - off : desc;
         const double end = double(tr.dev_end) * ns_per_tick - off;
         seg[0].push_back((double(tr.host_post_ns) - double(a)) * 1e-3);
         seg[1].push_back((take - double(tr.host_post_ns)) * 1e-3);
         seg[2].push_back((fence - take) * 1e-3);
         seg[3].push_back((desc - fence) * 1e-3);
-        seg[4].push_back((end - desc) * 1e-3);
-        seg[5].push_back((double(tr.host_seen_ns) - end) * 1e-3);
-        seg[6].push_back((double(b) - double(tr.host_seen_ns)) * 1e-3);
-        seg[7].push_back(double(b - a) * 1e-3);
+        seg[4].push_back((loaded - desc) * 1e-3);
+        seg[5].push_back((end - loaded) * 1e-3);
+        seg[6].push_back((double(tr.host_seen_ns) - end) * 1e-3);
+        seg[7].push_back((double(b) - double(tr.host_seen_ns)) * 1e-3);
+        seg[8].push_back(double(b - a) * 1e-3);
     }
     const double dt = double(mono_ns() - t_start) * 1e-9;
-    const char *names[8] = {"pre", "poll", "fence", "desc", "code", "complete", "post", "total"};
+    const char *names[9] = {"pre", "poll", "fence", "desc", "load", "code", "complete", "post", "total"};
     printf("{\"bench\": \"queue_latency\", \"family\": \"%s\", \"k\": %u, \"m\": %u, \"chunk\": %u, \"outputs\": %u, "
            "\"registered\": %d, \"calls\": %d, \"traced\": %zu, \"calls_per_s\": %.1f, \"clock_window_us\": %.3f",
-           argv[1], k, m, cs, nd, reg ? 1 : 0, calls, seg[7].size(), calls / dt, window * 1e-3);
-    for (int i = 0; i < 8; ++i)
+           argv[1], k, m, cs, nd, reg ? 1 : 0, calls, seg[8].size(), calls / dt, window * 1e-3);
+    for (int i = 0; i < 9; ++i)
         printf(", \"%s_us\": [%.3f, %.3f]", names[i], pct(seg[i], 0.5), pct(seg[i], 0.9));
     printf("}\n");
     if (reg) mec_host_unregister(slab);
