@@ -237,8 +237,8 @@ __device__ __forceinline__ void mark_active(uint64_t *act) {
 // or the masks (bitmatrix); a job's own share is a prefix of that payload,
 // but the whole of it is read in the same round trip as the rest
 constexpr uint32_t kQHeadWords = 8 + 2 * (kQMaxSrc + kQMaxDst);
-constexpr uint32_t kQDescWords = kQHeadWords + kQMaxSrc * kQBmRows / 4;  // >= the tables' kQMaxDst * kQMaxSrc * 5
-static_assert(kQMaxSrc * kQBmRows / 4 >= kQMaxDst * kQMaxSrc * 5, "descriptor LDS holds the tables");
+constexpr uint32_t kQDescWords = kQHeadWords + kQMaxDst * kQMaxSrc * 5;  // the tables outsize the masks
+static_assert(kQMaxDst * kQMaxSrc * 5 >= kQMaxSrc * kQBmRows / 4, "descriptor LDS holds the masks");
 static_assert(kQHeadWords % 4 == 0, "16-byte descriptor loads");
 // dwords of a job's descriptor: the head, then its tables / masks
 __device__ __forceinline__ uint32_t desc_words(uint32_t ns, uint32_t nd, bool bitmatrix) {

@@ -68,18 +68,12 @@ for step in "$@"; do
         wide) run wide_ab 600 python tools/wide_ab.py --steps 10 ;;
         server) run server_pattern 900 bash tools/server_pattern.sh ;;
         latency)
-            for args in "rs 8 2 4096 20000 1 1" "rs 8 2 4096 20000 0 1" "rs 4 2 4096 20000 1 1" "rs 10 4 65536 5000 1 1" \
-                        "cauchy 4 2 4096 20000 1 1" "rs 8 2 4096 20000 1 2"; do
-                run "latency_$(echo $args | tr ' ' _)" 120 tools/queue_latency $args
-            done
-            grep -h '^{' "$OUT"/latency_*.log > "$OUT/latency.jsonl" ;;
-        widepmc)
-            for sh in 0 1; do
-                for mode in wide split; do
-                    for ctr in FETCH_SIZE WRITE_SIZE; do
-                        run "pmc_wide_${sh}_${mode}_${ctr}" 300 rocprofv3 --pmc $ctr --output-format csv \
-                            -d "$OUT/pmc_wide_${sh}_${mode}_${ctr}" -o run -- python3 tools/wide_ab.py --mode $mode --shape $sh --steps 5 --warmup 1
-                    done
+            for env in ${LAT_ENVS:-"MEC_QUEUE_TIMEOUT_MS=5000"}; do
+                for args in ${LAT_ARGS:-"rs 8 2 4096 20000 1 1" "rs 8 2 4096 20000 0 1" "rs 4 2 4096 20000 1 1" \
+                            "rs 10 4 65536 5000 1 1" "cauchy 4 2 4096 20000 1 1" "rs 8 2 4096 20000 1 2"}; do
+                    tag="$(echo $env $args | tr ' =' '__')"
+                    run "latency_$tag" 120 env $env tools/queue_latency $args
+                    sed "s/^{/{\"env\": \"$env\", /" "$OUT/latency_$tag.log" | grep '^{' >> "$OUT/latency.jsonl"
                 done
             done ;;
         *) echo "unknown step $step"; exit 2 ;;
