@@ -67,10 +67,17 @@ for step in "$@"; do
             done ;;
         wide) run wide_ab 600 python tools/wide_ab.py --steps 10 ;;
         server) run server_pattern 900 bash tools/server_pattern.sh ;;
+        mixed)
+            for w in 1 4 16; do
+                run "mixed_w$w" 120 tools/mixed_ab 1024 $w 3 32
+            done
+            grep -h '^{' "$OUT"/mixed_w*.log > "$OUT/mixed.jsonl" ;;
         latency)
-            for env in ${LAT_ENVS:-"MEC_QUEUE_TIMEOUT_MS=5000"}; do
-                for args in ${LAT_ARGS:-"rs 8 2 4096 20000 1 1" "rs 8 2 4096 20000 0 1" "rs 4 2 4096 20000 1 1" \
-                            "rs 10 4 65536 5000 1 1" "cauchy 4 2 4096 20000 1 1" "rs 8 2 4096 20000 1 2"}; do
+            for env in ${LAT_ENVS:-MEC_QUEUE_TIMEOUT_MS=5000}; do  # ','-separated settings per run
+                for a in ${LAT_ARGS:-rs,8,2,4096,20000,1,1 rs,8,2,4096,20000,0,1 rs,4,2,4096,20000,1,1 \
+                         rs,10,4,65536,5000,1,1 cauchy,4,2,4096,20000,1,1 rs,8,2,4096,20000,1,2}; do
+                    args="$(echo $a | tr , ' ')"
+                    env=$(echo $env | tr , ' ')
                     tag="$(echo $env $args | tr ' =' '__')"
                     run "latency_$tag" 120 env $env tools/queue_latency $args
                     sed "s/^{/{\"env\": \"$env\", /" "$OUT/latency_$tag.log" | grep '^{' >> "$OUT/latency.jsonl"
