@@ -155,7 +155,6 @@ struct HostQueue {
     uint64_t idle_ticks = 0, timeout_ms = 5000;
     std::atomic<bool> *busy = nullptr;
     std::atomic<bool> trace{false};   // mec_queue_trace_enable
-    bool wt = false;                  // queue_kernel<true>: write-through outputs, relaxed done word
     hipStream_t stream = nullptr;
     std::mutex mu;  // launches
     std::atomic<uint64_t> calls{0}, launches{0};

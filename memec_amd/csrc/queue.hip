@@ -91,10 +91,7 @@ __device__ __forceinline__ void st_part(uint8_t *p, const u32x4 &v, uint32_t n) 
 // One 16-byte unit (FULL) or the n-byte tail at byte offset off of every
 // chunk: acc[r] (^)= sum_j coef[r][j] * src_j.  Source loads are issued in
 // groups of kQBatch back to back, one PCIe round trip per group.
-// WT: output stores write through (sc0 sc1 buffer stores), so the done
-// word needs no release (no L2 write-back) after the stores' acks
-constexpr int kAuxWT = 1 | 16;
-template <bool FULL, bool WT>
+template <bool FULL>
 __device__ __forceinline__ void code_unit(const uint64_t *addr, const uint32_t *tab, uint32_t ns, uint32_t nd,
                                           uint32_t acc_in, uint64_t off, uint32_t n, uint64_t *t_loaded = nullptr) {
     auto ld = [&](uint64_t p) {
@@ -133,11 +130,7 @@ __device__ __forceinline__ void code_unit(const uint64_t *addr, const uint32_t *
     for (int r = 0; r < int(kQMaxDst); ++r) {
         const uint64_t d = addr[kQMaxSrc + r];
         if (uint32_t(r) >= nd || !d) continue;
-        if constexpr (FULL && WT)
-            __builtin_amdgcn_raw_buffer_store_b128(
-                acc[r], __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void *>(d), 0, 0x7fffffff, 0x00020000),
-                uint32_t(off), 0, kAuxWT);
-        else if constexpr (FULL) *reinterpret_cast<u32x4 *>(d + off) = acc[r];
+        if constexpr (FULL) *reinterpret_cast<u32x4 *>(d + off) = acc[r];
         else st_part(reinterpret_cast<uint8_t *>(d + off), acc[r], n);
     }
 }
@@ -261,7 +254,6 @@ __device__ __forceinline__ uint32_t desc_words(uint32_t ns, uint32_t nd, bool bi
 // the other parts leave only after that, having run every job part 0 took
 // — so a job is run by all of a slot's parts or by none (a withdrawn job
 // is never taken, queue_try).
-template <bool WT>
 __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t *ctl, uint64_t *act, uint64_t *link,
                                                          uint64_t epoch, uint64_t idle_ticks, uint32_t nthr,
                                                          uint32_t nslots, uint32_t parts, uint32_t bitmatrix) {
@@ -367,10 +359,9 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             // this part's units: passes of nthr units, part-th of every parts
             const uint32_t full = bytes / 16, me = part * nthr + t, step = parts * nthr;
             for (uint32_t u = me; u < full; u += step)
-                code_unit<true, WT>(addr, tab, ns, nd, acc_in, uint64_t(u) * 16, 16,
-                                    traced && u == me ? &t_loaded : nullptr);
+                code_unit<true>(addr, tab, ns, nd, acc_in, uint64_t(u) * 16, 16, traced && u == me ? &t_loaded : nullptr);
             if (bytes % 16 && me == full % step)  // the partial last unit
-                code_unit<false, WT>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
+                code_unit<false>(addr, tab, ns, nd, acc_in, uint64_t(full) * 16, bytes % 16);
         } else {
             const uint32_t me = part * nthr + t, step = parts * nthr;
             switch (w) {  // uniform
@@ -403,12 +394,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
             __hip_atomic_store(&s->trace[4], t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (t == 0) {
-            // WT byte-wise jobs with no partial unit: every output byte was a
-            // write-through store, acknowledged before the barrier
-            if (WT && w == 0 && bytes % 16 == 0)
-                __hip_atomic_store(&s->done[part], last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            else
-                __hip_atomic_store(&s->done[part], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&s->done[part], last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             if (part == 0) mark_active(act + si);
         }
     }
@@ -450,14 +436,9 @@ int queue_launch(mec_ctx *c, HostQueue *q) {
     DeviceGuard dg(c->device);
     __atomic_store_n(q->ctl_host + kQCtlExit, 0u, __ATOMIC_RELEASE);
     ++q->epoch;
-    if (q->wt)
-        hipLaunchKernelGGL(queue_kernel<true>, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev,
-                           q->ctl_dev, q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts,
-                           c->byte_wise() ? 0u : 1u);
-    else
-        hipLaunchKernelGGL(queue_kernel<false>, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev,
-                           q->ctl_dev, q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts,
-                           c->byte_wise() ? 0u : 1u);
+    hipLaunchKernelGGL(queue_kernel, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev, q->ctl_dev,
+                       q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts,
+                       c->byte_wise() ? 0u : 1u);
     HIP_TRY(hipGetLastError());
     q->launches++;
     return MEC_OK;
@@ -523,7 +504,6 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     q->solo_max = uint32_t(env_u64("MEC_QUEUE_SOLO_MAX", q->max_chunk));
     q->idle_ticks = env_u64("MEC_QUEUE_IDLE_MS", 50) * 100000ull;  // s_memrealtime: 100 MHz
     q->timeout_ms = env_u64("MEC_QUEUE_TIMEOUT_MS", 5000);
-    q->wt = env_u64("MEC_QUEUE_WT", 0) != 0;  // experiment: write-through outputs, relaxed done
     // workgroups per slot: one per MEC_QUEUE_PART_THREADS units (default
     // kQThreads: a 16 KiB pass of 16-byte units), at most kQMaxParts;
     // MEC_QUEUE_PARTS sets the count directly (A/Bs)
@@ -541,7 +521,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     // launches beside it (calls beyond the slots, batches) keep CUs to run on
     {
         int per_cu = 0, cus = 0;
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_kernel<false>, int(q->threads), 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, queue_kernel, int(q->threads), 0));
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
         const uint32_t cap = uint32_t(std::max(1, per_cu * cus / 2)) / q->parts;
         slots = std::max<uint32_t>(1, std::min(slots, cap));

@@ -83,6 +83,15 @@ for step in "$@"; do
                     sed "s/^{/{\"env\": \"$env\", /" "$OUT/latency_$tag.log" | grep '^{' >> "$OUT/latency.jsonl"
                 done
             done ;;
+        widepmc)
+            for sh in ${WIDE_SHAPES:-0 1}; do
+                for mode in wide split; do
+                    for ctr in FETCH_SIZE WRITE_SIZE; do
+                        run "pmc_wide_${sh}_${mode}_${ctr}" 300 rocprofv3 --pmc $ctr --output-format csv \
+                            -d "$OUT/pmc_wide_${sh}_${mode}_${ctr}" -o run -- python3 tools/wide_ab.py --mode $mode --shape $sh --steps 5 --warmup 1
+                    done
+                done
+            done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done
