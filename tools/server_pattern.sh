@@ -18,7 +18,8 @@ g++ -std=c++11 -O2 -Wall -Imemec_amd/csrc/coding -Iinclude tools/coding_bench.cc
 SECS=${SECS:-2}
 J=$OUT/server_pattern.jsonl
 : > "$J"
-for cfg in ${CFGS:-"rs 4 2 4096" "rs 8 2 4096" "cauchy 4 2 4096" "rs 10 4 65536"}; do
+for c in ${CFGS:-rs,4,2,4096 rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536}; do  # scheme,k,m,chunk
+  cfg="$(echo $c | tr , ' ')"
   for mode in seal delta decode; do
     for w in ${WORKERS:-1 4 16}; do
       timeout -k 10 60 oracle/_ref/coding_bench_ref $cfg $w $SECS $mode >> "$J" || exit $?
