@@ -50,7 +50,6 @@ def run(mode, steps, warmup, shapes):
             step = lambda: c.decode(st, present)  # noqa: E731
             alg = (k + m) * cs * n
             result = lambda: st[:, erased]  # noqa: E731
-        del data
         arms = {}
         for arm in (["wide", "split"] if mode == "both" else [mode]):
             memec_amd.set_knob("MEC_WIDE", None if arm == "wide" else "0")
