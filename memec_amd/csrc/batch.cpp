@@ -294,8 +294,10 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
                const uint16_t *pat, uint32_t n, hipStream_t st, bool mapped_tables = false, bool device_mem = true) {
     if (M.ssel.empty() || M.rows() == 0 || n == 0) return MEC_OK;
     // a single map with no skipped stripe runs from kernel arguments;
-    // anything else through per-stripe descriptors
-    bool single = M.ssel.size() == 1;
+    // anything else through per-stripe descriptors (and byte-wise maps with
+    // more than 4 outputs too: the descriptor kernel codes every row group
+    // from one read of the sources)
+    bool single = M.ssel.size() == 1 && !(c->byte_wise() && M.rows() > size_t(kMaxRows));
     if (single && pat)
         for (uint32_t s = 0; s < n && single; ++s) single = pat[s] == 0;
     std::vector<uint32_t> descs;
@@ -374,15 +376,22 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
     L.n_stripes = n;
     L.k = int(M.K);
     L.accumulate = M.accumulate;
+    if (c->byte_wise()) {  // every row group in one launch (rows past a map's own are kNoRow)
+        L.rows = int(std::min<size_t>(kMaxRows, rows));
+        L.desc = dev + offs[3];
+        L.desc_dw = desc_dw;
+        L.groups = uint32_t(groups);
+        L.group_maps = uint32_t(nm);
+        L.w = 0;
+        L.len = c->cs;
+        HIP_TRY(launch_gf8_gather(L, st));
+        return MEC_OK;
+    }
     for (size_t g = 0; g < groups; ++g) {
         L.rows = int(std::min<size_t>(kMaxRows, rows - g * kMaxRows));
         L.desc = dev + offs[3] + g * nm * desc_dw * sizeof(uint32_t);
         L.desc_dw = desc_dw;
-        if (c->byte_wise()) {
-            L.w = 0;
-            L.len = c->cs;
-            HIP_TRY(launch_gf8_gather(L, st));
-        } else {
+        {
             L.w = int(c->w);
             L.len = c->packet;
             HIP_TRY(launch_bm_gather(L, st));

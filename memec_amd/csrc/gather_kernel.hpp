@@ -31,6 +31,9 @@ struct GatherParams {
     uint32_t desc_dw;
     uint32_t sstride, dstride;
     uint32_t s0, units, tiles, k, accumulate;
+    // gf8: row groups coded in this launch from one read of the sources;
+    // group g's descriptor of map d at desc + (g * group_maps + d) * desc_dw
+    uint32_t groups, group_maps;
 };
 
 __device__ __forceinline__ uint32_t gather_desc(const GatherParams &p, uint32_t s) {
@@ -80,29 +83,70 @@ __device__ __forceinline__ bool gather_prologue(const GatherParams &p, uint32_t 
     return true;
 }
 
-template <int K, int R>
+// MG = false: one row group per launch (m <= 4; the kernel before round 4).
+// MG = true (R = 4 only): every row group of the descriptors in one launch,
+// the k sources read once (m > 4) — a separate instantiation because the
+// group loop's barriers keep lanes past the chunk alive and cost ~20-30
+// VGPRs, which the common m <= 4 launches should not pay.
+template <int K, int R, bool MG>
 __global__ __launch_bounds__(kThreads) void gf8_gather_kernel(const GatherParams p) {
     constexpr int NDW = kGf8DescHead + R * K * 8;
     __shared__ uint32_t dsc[NDW];
     __shared__ uint64_t ptr[K + R];
     const uint32_t local = blockIdx.x / p.tiles;
-    if (!gather_prologue<NDW, K, R>(p, p.s0 + local, K, dsc, ptr, 8, 16)) return;
+    const uint32_t s = p.s0 + local;
+    if (!gather_prologue<NDW, K, R>(p, s, K, dsc, ptr, 8, 16)) return;
     const uint32_t u = (blockIdx.x - local * p.tiles) * kThreads + threadIdx.x;
-    if (u >= p.units) return;
-    const uint32_t off = u * 16;
-
-    u32x4 d[K];
+    if constexpr (!MG) {
+        if (u >= p.units) return;
+        const uint32_t off = u * 16;
+        u32x4 d[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j) d[j] = buf_ld<u32x4>(chunk_rsrc(uniform64(ptr[j]), p.chunk), off, true);
-    __amdgpu_buffer_rsrc_t dr[R];
+        for (int j = 0; j < K; ++j) d[j] = buf_ld<u32x4>(chunk_rsrc(uniform64(ptr[j]), p.chunk), off, true);
+        __amdgpu_buffer_rsrc_t dr[R];
 #pragma unroll
-    for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(uniform64(ptr[K + i]), p.chunk);
-    u32x4 acc[R];
+        for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(uniform64(ptr[K + i]), p.chunk);
+        u32x4 acc[R];
 #pragma unroll
-    for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
-    gf8_apply<K, R, kGf8Dense>(d, acc, dsc + kGf8DescHead + opaque_zero());
+        for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
+        gf8_apply<K, R, kGf8Dense>(d, acc, dsc + kGf8DescHead + opaque_zero());
 #pragma unroll
-    for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
+        for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
+    } else {
+        // lanes past the chunk stay for the group barriers, without memory ops
+        const bool live = u < p.units;
+        const uint32_t off = live ? u * 16 : 0u;
+        u32x4 d[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            d[j] = live ? buf_ld<u32x4>(chunk_rsrc(uniform64(ptr[j]), p.chunk), off, true) : u32x4{0, 0, 0, 0};
+        for (uint32_t g = 0;;) {  // uniform
+            __amdgpu_buffer_rsrc_t dr[R];
+#pragma unroll
+            for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(live ? uniform64(ptr[K + i]) : 0, p.chunk);
+            u32x4 acc[R];
+#pragma unroll
+            for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
+            gf8_apply<K, R, kGf8Dense>(d, acc, dsc + kGf8DescHead + opaque_zero());
+#pragma unroll
+            for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
+            if (++g >= p.groups) break;
+            // next group: its descriptor (output rows, tables), its output pointers
+            __syncthreads();
+            const uint32_t *D = p.desc + (size_t(g) * p.group_maps + gather_desc(p, s)) * p.desc_dw;
+            for (int q = threadIdx.x; q < NDW; q += kThreads) dsc[q] = D[q];
+            __syncthreads();
+            if (threadIdx.x < R) {
+                const uint32_t sel = (dsc[16] >> (8 * threadIdx.x)) & 0xffu;
+                ptr[K + threadIdx.x] = sel == kNoRow ? 0 : p.dtab[uint64_t(s) * p.dstride + sel];
+            }
+            __syncthreads();
+            // the sources "change" (an empty asm): their bit fields are not
+            // hoisted out of the group loop (as gf8_mg_kernel)
+#pragma unroll
+            for (int j = 0; j < K; ++j) asm volatile("" : "+v"(d[j]));
+        }
+    }
 }
 
 template <int W, int R>
@@ -182,6 +226,8 @@ inline GatherParams gather_params(const GatherLaunch &L, const Geometry &g) {
     p.tiles = g.tiles;
     p.k = uint32_t(L.k);
     p.accumulate = L.accumulate ? 1u : 0u;
+    p.groups = L.groups ? L.groups : 1u;
+    p.group_maps = L.group_maps;
     return p;
 }
 
@@ -193,12 +239,27 @@ hipError_t run_gf8_gather(const GatherLaunch &L, hipStream_t stream) {
         for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
             p.s0 = s0;
-            hipLaunchKernelGGL((gf8_gather_kernel<K, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            if constexpr (R == kMaxRows) {
+                if (p.groups > 1)
+                    hipLaunchKernelGGL((gf8_gather_kernel<K, R, true>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+                else
+                    hipLaunchKernelGGL((gf8_gather_kernel<K, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            } else {
+                if (p.groups > 1) return hipErrorInvalidValue;  // multi-group launches run 4 rows per group
+                hipLaunchKernelGGL((gf8_gather_kernel<K, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
+            }
             hipError_t e = hipGetLastError();
             if (e != hipSuccess) return e;
         }
     }
-    if (L.len % 16) return launch_gather_tail(L, false, uint64_t(g.units) * 16, stream);
+    if (L.len % 16)  // the tail, one launch per row group
+        for (uint32_t grp = 0; grp < std::max(1u, L.groups); ++grp) {
+            GatherLaunch Lg = L;
+            Lg.desc = static_cast<const uint8_t *>(L.desc) + size_t(grp) * L.group_maps * L.desc_dw * sizeof(uint32_t);
+            Lg.groups = 1;
+            hipError_t e = launch_gather_tail(Lg, false, uint64_t(g.units) * 16, stream);
+            if (e != hipSuccess) return e;
+        }
     return hipSuccess;
 }
 

@@ -101,6 +101,9 @@ struct GatherLaunch {
     int w;                 // bitmatrix field width
     uint64_t len;          // gf8: bytes per chunk; bitmatrix: packet bytes
     bool accumulate;       // XOR into outputs
+    // gf8 only: row groups of kMaxRows coded in one launch (0/1 = this
+    // group only); group g's descriptors at desc + g * group_maps * desc_dw
+    uint32_t groups, group_maps;
 };
 
 // Host side of a multi-group launch: rows (> kMaxRows) outputs at dst_off,

@@ -159,3 +159,72 @@ def test_wide_update_linearity(fam):
         torch.cuda.synchronize()
         assert torch.equal(par, par2), (fam, k, m)
         c.close()
+
+
+# ---- pointer batches (gathered kernels): every row group in one launch ----
+
+from test_gpu_batch import Slab, chunk_of, random_patterns, zeros  # noqa: E402
+
+
+@pytest.mark.parametrize("mem", ["device", "host"])
+@pytest.mark.parametrize("fam", FAMS)
+def test_wide_encode_batch_scattered(fam, mem):
+    """mec_encode_batch with 7 parities (row groups of 4 + 3), scattered
+    ChunkPool-like slots, Coding::zeros columns and unwanted parities."""
+    k, m, cs, n = 10, 7, 1024, 24
+    if fam == "cauchy" and not ok_shape(fam, k, m, cs):
+        pytest.skip("no Cauchy w")
+    rng = np.random.default_rng(17)
+    slots = rng.permutation(n * (k + m))
+    slab = Slab(n * (k + m), cs, 8, mem == "device", 77)
+    before = slab.snapshot()
+    dptr, pptr, want = [], [], []
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        zero_cols = set(rng.choice(k, size=int(rng.integers(0, 4)), replace=False).tolist())
+        wanted = [bool(rng.integers(0, 4)) for _ in range(m)] if s % 2 else [True] * m
+        dptr += [0 if j in zero_cols else slab.addr(row[j]) for j in range(k)]
+        pptr += [slab.addr(row[k + i]) if wanted[i] else 0 for i in range(m)]
+        data = [zeros(cs) if j in zero_cols else chunk_of(before, slab, row[j]).copy() for j in range(k)]
+        want.append((row, wanted, O.encode(fam, k, m, data, cs)))
+    c = Codec(fam, k, m, cs)
+    c.encode_batch(dptr, pptr, mem=mem)
+    after = slab.snapshot()
+    for s, (row, wanted, par) in enumerate(want):
+        for i in range(m):
+            got = chunk_of(after, slab, row[k + i])
+            ref = par[i] if wanted[i] else chunk_of(before, slab, row[k + i])
+            assert np.array_equal(got, ref), (fam, mem, s, i, wanted[i])
+    c.close()
+
+
+@pytest.mark.parametrize("mem", ["device", "host"])
+@pytest.mark.parametrize("fam", FAMS)
+def test_wide_decode_batch_mixed_patterns(fam, mem):
+    """mec_decode_batch, RS/CRS(8,6): every stripe its own pattern of 0..6
+    erasures (and some with 7: too many), random non-codeword stripes."""
+    k, m, cs, n = 8, 6, 1024, 40
+    if fam == "cauchy" and not ok_shape(fam, k, m, cs):
+        pytest.skip("no Cauchy w")
+    rng = np.random.default_rng(23)
+    slots = rng.permutation(n * (k + m))
+    slab = Slab(n * (k + m), cs, 8, mem == "device", 4242)
+    before = slab.snapshot()
+    pats = random_patterns(rng, n, k, m)
+    ptrs, masks = [], []
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        ptrs += [slab.addr(i) for i in row]
+        masks.append(sum(1 << i for i in range(k + m) if i not in pats[s]))
+    c = Codec(fam, k, m, cs)
+    res = c.decode_batch(ptrs, masks, mem=mem)
+    after = slab.snapshot()
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        chunks = [chunk_of(before, slab, i).copy() for i in row]
+        if len(pats[s]) <= m and pats[s]:
+            assert res[s] == 0
+            assert O.decode(fam, k, m, chunks, pats[s], cs) == 0
+        for i in range(k + m):
+            assert np.array_equal(chunk_of(after, slab, row[i]), chunks[i]), (fam, mem, s, pats[s], i)
+    c.close()
