@@ -20,7 +20,7 @@ SYMBOLS = (
     "mec_encode_update", "mec_xor", "mec_fill_random", "mec_encode_host", "mec_decode_host",
     "mec_encode_update_host", "mec_encode_host_batch", "mec_host_register", "mec_host_unregister",
     "mec_encode_batch", "mec_decode_batch", "mec_encode_update_batch", "mec_set_coalescing", "mec_set_host_queue", "mec_get_stats",
-    "mec_set_probe", "mec_set_knob",
+    "mec_set_probe", "mec_set_knob", "mec_queue_trace_enable", "mec_queue_last_trace",
 )
 MEM_DEVICE, MEM_HOST = 0, 1
 
