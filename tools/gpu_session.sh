@@ -68,6 +68,7 @@ for step in "$@"; do
         wide) run wide_ab 600 python tools/wide_ab.py --steps 10 ;;
         server) run server_pattern 900 bash tools/server_pattern.sh ;;
         stagger) run stagger_probe 300 tools/stagger_probe 4096 3 ;;
+        wider8) run wide_r8_probe 300 tools/wide_r8_probe 16384 3 ;;
         mixed)
             for w in 1 4 16; do
                 run "mixed_w$w" 120 tools/mixed_ab 1024 $w 3 32
