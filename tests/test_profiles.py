@@ -2,7 +2,7 @@
 
 bench.py's `roofline.traffic` is read from profiles/pmc_<config>.json, and
 DESIGN quotes the default command's line next to the rocprofv3 kernel
-averages of the same run (profiles/r03/final/).  These checks keep those
+averages of the same run (profiles/rNN/final/, the newest round).  These checks keep those
 files consistent: PMC traffic equals the algorithmic bytes, and every timed
 config's kernel_ms in the line under the profiler matches the profiler's own
 average for that kernel.
@@ -15,7 +15,8 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-FINAL = os.path.join(ROOT, "profiles", "r03", "final")
+# the newest round's round-final profile (profiles/rNN/final/)
+FINAL = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "final")))[-1]
 
 
 def _line(path):
