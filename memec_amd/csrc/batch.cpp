@@ -165,10 +165,15 @@ struct MapSet {
 };
 
 // Descriptor blobs [row group][map] (layout in kernels.hpp).
+// Rows per descriptor group: 4 byte-wise (the gf8 kernels' R; more groups
+// run in the same launch), 8 bitmatrix (a launch keeps 8 x w packet slices).
+size_t group_rows(const mec_ctx *c) { return c->byte_wise() ? size_t(kMaxRows) : size_t(kBmGatherRows); }
+
 size_t build_descs(const mec_ctx *c, const MapSet &M, std::vector<uint32_t> &out, uint32_t &desc_dw) {
-    const size_t groups = (M.rows() + kMaxRows - 1) / kMaxRows, nm = M.ssel.size();
+    const size_t GR = group_rows(c);
+    const size_t groups = (M.rows() + GR - 1) / GR, nm = M.ssel.size();
     const uint32_t K = M.K;
-    desc_dw = c->byte_wise() ? uint32_t(kGf8DescHead + kMaxRows * K * 8) : uint32_t(kBmDescHead + kMaxSrc * c->w);
+    desc_dw = c->byte_wise() ? uint32_t(kGf8DescHead + kMaxRows * K * 8) : uint32_t(kBmDescHead + kMaxSrc * 2 * c->w);
     out.assign(groups * nm * desc_dw, 0);
     auto put_byte = [](uint32_t *w, size_t idx, uint8_t v) { w[idx / 4] |= uint32_t(v) << (8 * (idx % 4)); };
     for (size_t g = 0; g < groups; ++g)
@@ -177,8 +182,8 @@ size_t build_descs(const mec_ctx *c, const MapSet &M, std::vector<uint32_t> &out
             const size_t nd = M.dsel[q].size();
             const uint32_t sel_dw = c->byte_wise() ? 8 : 0, dsel_dw = c->byte_wise() ? 16 : 8;
             for (uint32_t j = 0; j < K; ++j) put_byte(D + sel_dw, j, M.ssel[q][j]);
-            for (int i = 0; i < kMaxRows; ++i) {
-                const size_t r = g * kMaxRows + i;
+            for (size_t i = 0; i < GR; ++i) {
+                const size_t r = g * GR + i;
                 put_byte(D + dsel_dw, i, r < nd ? M.dsel[q][r] : kNoRow);
             }
             if (c->byte_wise()) {
@@ -200,14 +205,14 @@ size_t build_descs(const mec_ctx *c, const MapSet &M, std::vector<uint32_t> &out
                 }
             } else {
                 const Field &f = Field::get(int(c->w));
-                for (int i = 0; i < kMaxRows; ++i) {
-                    const size_t r = g * kMaxRows + i;
+                for (size_t i = 0; i < GR; ++i) {
+                    const size_t r = g * GR + i;
                     if (r >= nd) continue;
                     for (uint32_t j = 0; j < K; ++j) {
                         uint8_t mask[8];
                         bit_block(f, M.coef[q][r * K + j], c->w, mask, 1);
                         for (uint32_t l = 0; l < c->w; ++l)
-                            put_byte(D + kBmDescHead + j * c->w, i * c->w + l, mask[l]);
+                            put_byte(D + kBmDescHead + j * 2 * c->w, i * c->w + l, mask[l]);
                     }
                 }
             }
@@ -297,7 +302,7 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
     // anything else through per-stripe descriptors (and byte-wise maps with
     // more than 4 outputs too: the descriptor kernel codes every row group
     // from one read of the sources)
-    bool single = M.ssel.size() == 1 && !(c->byte_wise() && M.rows() > size_t(kMaxRows));
+    bool single = M.ssel.size() == 1 && M.rows() <= size_t(kMaxRows);
     if (single && pat)
         for (uint32_t s = 0; s < n && single; ++s) single = pat[s] == 0;
     std::vector<uint32_t> descs;
@@ -387,8 +392,8 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
         HIP_TRY(launch_gf8_gather(L, st));
         return MEC_OK;
     }
-    for (size_t g = 0; g < groups; ++g) {
-        L.rows = int(std::min<size_t>(kMaxRows, rows - g * kMaxRows));
+    for (size_t g = 0; g < groups; ++g) {  // bitmatrix: groups of up to 8 outputs
+        L.rows = int(std::min<size_t>(kBmGatherRows, rows - g * kBmGatherRows));
         L.desc = dev + offs[3] + g * nm * desc_dw * sizeof(uint32_t);
         L.desc_dw = desc_dw;
         {

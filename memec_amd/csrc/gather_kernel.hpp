@@ -76,7 +76,7 @@ __device__ __forceinline__ bool gather_prologue(const GatherParams &p, uint32_t 
         const uint32_t sel = (dsc[sel_dw + t / 4] >> (8 * (t % 4))) & 0xffu;
         ptr[t] = p.stab[uint64_t(s) * p.sstride + sel];
     } else if (t >= 64 && t < 64 + R) {
-        const uint32_t sel = (dsc[dsel_dw] >> (8 * (t - 64))) & 0xffu;
+        const uint32_t sel = (dsc[dsel_dw + (t - 64) / 4] >> (8 * ((t - 64) % 4))) & 0xffu;
         ptr[KMAX + t - 64] = sel == kNoRow ? 0 : p.dtab[uint64_t(s) * p.dstride + sel];
     }
     __syncthreads();
@@ -155,7 +155,8 @@ __global__ __launch_bounds__(kThreads) void bm_gather_kernel(const GatherParams 
     constexpr int UB = 4 * VW;
     constexpr int ROWS = R * W;
     constexpr int MW = (ROWS + 3) / 4;  // mask dwords used per source (of W stored)
-    constexpr int NDW = kBmDescHead + kMaxSrc * W;
+    constexpr int MS = 2 * W;  // mask dwords per source (kBmGatherRows rows of W bytes)
+    constexpr int NDW = kBmDescHead + kMaxSrc * MS;
     typedef typename VecT<VW>::type vec;
     __shared__ uint32_t dsc[NDW];
     __shared__ uint64_t ptr[kMaxSrc + R];
@@ -189,7 +190,7 @@ __global__ __launch_bounds__(kThreads) void bm_gather_kernel(const GatherParams 
         }
         uint32_t mw[MW];
 #pragma unroll
-        for (int q = 0; q < MW; ++q) mw[q] = uniform32(mt[j * W + q]);
+        for (int q = 0; q < MW; ++q) mw[q] = uniform32(mt[j * MS + q]);
 #pragma unroll
         for (int r = 0; r < ROWS; ++r) {
             const uint32_t mb = (mw[r / 4] >> (8 * (r % 4))) & 0xffu;
@@ -287,7 +288,7 @@ hipError_t run_bm_gather(const GatherLaunch &L, hipStream_t stream) {
 #define MEC_GG8_INSTANTIATE_HI(R) MEC_FOR_K_HI(MEC_GG8_ONE, R)
 #define MEC_GBM_ONE(W, R) template hipError_t run_bm_gather<W, R>(const GatherLaunch &, hipStream_t);
 #define MEC_GBM_EXT(W, R) extern template hipError_t run_bm_gather<W, R>(const GatherLaunch &, hipStream_t);
-#define MEC_GBM_INSTANTIATE_W(W) MEC_FOR_R4(MEC_GBM_ONE, W)
+#define MEC_GBM_INSTANTIATE_W(W) MEC_FOR_R8(MEC_GBM_ONE, W)
 
 }  // namespace detail
 }  // namespace mec

@@ -47,7 +47,7 @@ MEC_FOR_K(MEC_GF8_EXT, 1) MEC_FOR_K(MEC_GF8_EXT, 2) MEC_FOR_K(MEC_GF8_EXT, 3) ME
 MEC_FOR_K(MEC_GFM_EXT, 3) MEC_FOR_K(MEC_GFM_EXT, 4)
 MEC_FOR_K(MEC_GG8_EXT, 1) MEC_FOR_K(MEC_GG8_EXT, 2) MEC_FOR_K(MEC_GG8_EXT, 3) MEC_FOR_K(MEC_GG8_EXT, 4)
 MEC_FOR_W(MEC_FOR_R8, MEC_BM_EXT)
-MEC_FOR_W(MEC_FOR_R4, MEC_GBM_EXT)
+MEC_FOR_W(MEC_FOR_R8, MEC_GBM_EXT)
 
 // Gathered tails: the < unit remainder of each region, one thread per
 // stripe, any k / rows / w, reading the descriptor blob directly.
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(kThreads) void gather_tail_kernel(const GatherParam
         return a ? load_partial(reinterpret_cast<const uint8_t *>(a) + off + extra, n) : u32x4{0, 0, 0, 0};
     };
     for (uint32_t i = 0; i < rows; ++i) {
-        const uint32_t sel = (D[dsel_dw] >> (8 * i)) & 0xffu;
+        const uint32_t sel = (D[dsel_dw + i / 4] >> (8 * (i % 4))) & 0xffu;
         if (sel == kNoRow || !drow[sel]) continue;
         uint8_t *q0 = reinterpret_cast<uint8_t *>(drow[sel]) + off;
         if (!bitmatrix) {
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kThreads) void gather_tail_kernel(const GatherParam
                 u32x4 acc = p.accumulate ? load_partial(q, n) : u32x4{0, 0, 0, 0};
                 for (uint32_t j = 0; j < p.k; ++j) {
                     const uint32_t r = i * w + l;
-                    const uint32_t mb = (D[kBmDescHead + j * w + r / 4] >> (8 * (r % 4))) & 0xffu;
+                    const uint32_t mb = (D[kBmDescHead + j * 2 * w + r / 4] >> (8 * (r % 4))) & 0xffu;
                     for (uint32_t x = 0; x < w; ++x)
                         if ((mb >> x) & 1u) acc ^= src(j, uint64_t(x) * p.packet);
                 }
@@ -420,9 +420,9 @@ const auto kGg8Table = make_gg8_table(std::make_index_sequence<kMaxK * kMaxRows>
 
 template <size_t... I>
 constexpr std::array<GatherFn, sizeof...(I)> make_gbm_table(std::index_sequence<I...>) {
-    return {{&run_bm_gather<int(I / kMaxRows) + 1, int(I % kMaxRows) + 1>...}};
+    return {{&run_bm_gather<int(I / kBmGatherRows) + 1, int(I % kBmGatherRows) + 1>...}};
 }
-const auto kGbmTable = make_gbm_table(std::make_index_sequence<8 * kMaxRows>{});
+const auto kGbmTable = make_gbm_table(std::make_index_sequence<8 * kBmGatherRows>{});
 
 // ---------------------------------------------------------------------------
 // XOR and fill
@@ -523,11 +523,11 @@ hipError_t launch_gf8_gather(const GatherLaunch &L, hipStream_t stream) {
 }
 
 hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream) {
-    if (L.k < 1 || L.k > kMaxK || L.rows < 1 || L.rows > kMaxRows || L.w < 1 || L.w > 8 || !L.stab || !L.dtab ||
-        !L.desc)
+    if (L.k < 1 || L.k > kMaxK || L.rows < 1 || L.rows > kBmGatherRows || L.w < 1 || L.w > 8 || !L.stab ||
+        !L.dtab || !L.desc)
         return hipErrorInvalidValue;
     if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
-    return kGbmTable[size_t(L.w - 1) * kMaxRows + size_t(L.rows - 1)](L, stream);
+    return kGbmTable[size_t(L.w - 1) * kBmGatherRows + size_t(L.rows - 1)](L, stream);
 }
 
 hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, hipStream_t stream) {

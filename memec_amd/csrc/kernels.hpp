@@ -82,12 +82,13 @@ constexpr uint16_t kSkipStripe = 0xFFFF;
 //      [8..15] ssel bytes, [16] dsel bytes (kNoRow = no output), then at
 //      kGf8DescHead + (i*K + j)*8 the v_perm tables t0 t1 u0 u1 v of
 //      coefficient (i, j);  desc_dw = kGf8DescHead + 4*K*8.
-//  bitmatrix (K sources, width w, 4 rows): [0..7] ssel bytes, [8] dsel bytes,
-//      then at kBmDescHead + j*w + q the mask bytes 4q..4q+3 of source j
-//      (byte i*w + l: bit x set <=> packet x feeds output i packet l);
-//      desc_dw = kBmDescHead + kMaxSrc*w.
+//  bitmatrix (K sources, width w, up to kMaxBmOut = 8 rows): [0..7] ssel
+//      bytes, [8..9] dsel bytes, then at kBmDescHead + j*2w + q the mask
+//      bytes 4q..4q+3 of source j (byte i*w + l: bit x set <=> packet x
+//      feeds output i packet l); desc_dw = kBmDescHead + kMaxSrc*2w.
 constexpr int kGf8DescHead = 32;
 constexpr int kBmDescHead = 16;
+constexpr int kBmGatherRows = 8;  // outputs per gathered bitmatrix launch (= kMaxBmOut)
 
 struct GatherLaunch {
     const uint64_t *stab;  // source pointer rows: stripe s at stab + s * sstride (0 = all-zero chunk)
