@@ -16,7 +16,8 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # the newest round's round-final profile (profiles/rNN/final/)
-FINAL = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "final")))[-1]
+# (none on the GPU box, where old rounds' profiles are not shipped: skip)
+FINAL = (sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "final"))) or [os.path.join(ROOT, "profiles", "none")])[-1]
 
 
 def _line(path):
