@@ -82,6 +82,7 @@ struct Arm {
     int s;       // kGf8Dense / kGf8Vand / kGf8Xor
     int sleep;
     bool rev;
+    int cap = 0;  // waves per CU; 0 = the product's rule (gf8_target_waves)
 };
 
 template <int S, int BT, int SLEEP, bool REV>
@@ -96,7 +97,11 @@ void launch_s(int sleep, bool rev, dim3 grid, uint32_t lds, const Gf8Params<K, R
         case 1: launch<S, BT, 0, true>(grid, lds, p); break;
         case 4: launch<S, BT, 2, false>(grid, lds, p); break;
         case 16: launch<S, BT, 8, false>(grid, lds, p); break;
+        case 32: launch<S, BT, 16, false>(grid, lds, p); break;
+        case 48: launch<S, BT, 24, false>(grid, lds, p); break;
         case 64: launch<S, BT, 32, false>(grid, lds, p); break;
+        case 65: launch<S, BT, 32, true>(grid, lds, p); break;
+        case 96: launch<S, BT, 48, false>(grid, lds, p); break;
         case 128: launch<S, BT, 64, false>(grid, lds, p); break;
         default: fprintf(stderr, "arm not instantiated\n"); exit(2);
     }
@@ -119,14 +124,17 @@ int main(int argc, char **argv) {
                                 {1, 103, 156, 151, 123, 187, 166, 175, 244, 83},
                                 {1, 220, 166, 123, 82, 143, 245, 40, 167, 122}};
     std::vector<Arm> arms = {
-        {"inplace_dec", true, kGf8Dense, 0, false},        {"inplace_dec_rev", true, kGf8Dense, 0, true},
-        {"inplace_dec_sleep2", true, kGf8Dense, 2, false}, {"inplace_dec_sleep8", true, kGf8Dense, 8, false},
-        {"inplace_dec_sleep32", true, kGf8Dense, 32, false}, {"inplace_dec_sleep64", true, kGf8Dense, 64, false},
-        {"inplace_twin", true, kGf8Xor, 0, false},         {"inplace_twin_sleep8", true, kGf8Xor, 8, false},
-        {"inplace_twin_sleep32", true, kGf8Xor, 32, false}, {"inplace_vand", true, kGf8Vand, 0, false},
-        {"split_enc", false, kGf8Vand, 0, false},           {"split_twin", false, kGf8Xor, 0, false},
-        {"split_twin_sleep8", false, kGf8Xor, 8, false},    {"split_twin_sleep32", false, kGf8Xor, 32, false},
-        {"split_dense", false, kGf8Dense, 0, false},        {"split_dense_sleep8", false, kGf8Dense, 8, false},
+        {"inplace_dec", true, kGf8Dense, 0, false},          {"inplace_dec_rev", true, kGf8Dense, 0, true},
+        {"inplace_dec_sleep16", true, kGf8Dense, 16, false}, {"inplace_dec_sleep24", true, kGf8Dense, 24, false},
+        {"inplace_dec_sleep32", true, kGf8Dense, 32, false}, {"inplace_dec_sleep48", true, kGf8Dense, 48, false},
+        {"inplace_dec_rev_sleep32", true, kGf8Dense, 32, true},
+        {"inplace_dec_cap12", true, kGf8Dense, 0, false, 12}, {"inplace_dec_cap14", true, kGf8Dense, 0, false, 14},
+        {"inplace_dec_cap12_sleep32", true, kGf8Dense, 32, false, 12},
+        {"inplace_twin", true, kGf8Xor, 0, false},           {"inplace_vand", true, kGf8Vand, 0, false},
+        {"inplace_vand_cap16", true, kGf8Vand, 0, false, 16},
+        {"split_enc", false, kGf8Vand, 0, false},             {"split_enc_cap16", false, kGf8Vand, 0, false, 16},
+        {"split_twin", false, kGf8Xor, 0, false},             {"split_twin_cap12", false, kGf8Xor, 0, false, 12},
+        {"split_dense", false, kGf8Dense, 0, false},          {"split_dense_cap12", false, kGf8Dense, 0, false, 12},
     };
     const double alg = double(n) * (K + R) * CS;
     for (int rd = 0; rd < rounds; ++rd) {
@@ -154,7 +162,8 @@ int main(int argc, char **argv) {
             p.s0 = 0;
             p.sgroup = stripe_group(CS, g.tiles, p.win > 1 ? n / p.win : n, p.win > 1, false, p.srun);
             const bool dense = a.s != kGf8Vand;
-            const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, ip, dense, false));
+            const uint32_t lds =
+                occupancy_lds(bt, bt, R * K * 32, a.cap ? uint32_t(a.cap) : gf8_target_waves(K, R, ip, dense, false));
             const dim3 grid(n * g.tiles);
             auto go = [&] {
                 if (bt == kWaveBlock) {
