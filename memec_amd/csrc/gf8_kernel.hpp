@@ -34,6 +34,7 @@ struct Gf8Params {
     uint32_t sstride, dstride, chunk, s0;
     uint32_t units, tiles, accumulate, win;
     uint32_t nstr, sgroup, srun;  // stripes in this launch, stripe group and run (stripe_tile)
+    uint32_t stagger;             // != 0: s_sleep(32) between the arithmetic and the stores
     int64_t src_off[K];
     int64_t dst_off[R];
     Gf8Coef coef[R][K];
@@ -200,6 +201,10 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
 #pragma unroll
     for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
     gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
+    // uniform; see gf8_stagger.  The branch is inside the asm: a C++ branch
+    // here splits the block and the compiler then keeps every bit field of
+    // the sources live across it (RS(10,4) dense 99 -> 272 VGPRs).
+    asm volatile("s_cmp_eq_u32 %0, 0\n\ts_cbranch_scc1 1f\n\ts_sleep 32\n1:" ::"s"(p.stagger) : "scc");
 #pragma unroll
     for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
 }
@@ -325,6 +330,7 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     p.nstr = 0;
     p.sgroup = 0;
     p.srun = 8;
+    p.stagger = 0;
     for (int j = 0; j < K; ++j) p.src_off[j] = L.src_off[j];
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int i = 0; i < R; ++i)
@@ -357,6 +363,7 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                 const bool in_place = p.win > 1;
                 const dim3 grid(ns * g.tiles), block(bt);
                 const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, in_place, !vand, L.accumulate));
+                p.stagger = L.probe ? 0u : gf8_stagger(R, in_place, !vand, L.accumulate);
                 if (L.probe) {
                     if (bt == kWaveBlock)
                         hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Xor, kWaveBlock>), grid, block, lds, stream, p);
@@ -426,6 +433,10 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
 #define MEC_GF8_INSTANTIATE_HI(R) MEC_FOR_K_HI(MEC_GF8_ONE, R)
 #define MEC_GFM_ONE(K, R) template hipError_t run_gf8_mg<K, R>(const Gf8MgLaunch &, hipStream_t);
 #define MEC_GFM_EXT(K, R) extern template hipError_t run_gf8_mg<K, R>(const Gf8MgLaunch &, hipStream_t);
+// the 8-row group instantiations, K = kMg8MinK..kMg8MaxK
+#define MEC_FOR_K8(X) \
+    X(12, 8) X(13, 8) X(14, 8) X(15, 8) X(16, 8) X(17, 8) X(18, 8) X(19, 8) X(20, 8)
+static_assert(kMg8MinK == 12 && kMg8MaxK == 20, "MEC_FOR_K8 lists K = 12..20");
 
 }  // namespace detail
 }  // namespace mec

@@ -44,7 +44,7 @@ template <int W, int R>
 hipError_t run_bm_gather(const GatherLaunch &L, hipStream_t stream);
 // instantiated in gf8_r*.hip, gg8_r*.hip, bm_w*.hip and gbm.hip, never here
 MEC_FOR_K(MEC_GF8_EXT, 1) MEC_FOR_K(MEC_GF8_EXT, 2) MEC_FOR_K(MEC_GF8_EXT, 3) MEC_FOR_K(MEC_GF8_EXT, 4)
-MEC_FOR_K(MEC_GFM_EXT, 3) MEC_FOR_K(MEC_GFM_EXT, 4)
+MEC_FOR_K(MEC_GFM_EXT, 3) MEC_FOR_K(MEC_GFM_EXT, 4) MEC_FOR_K8(MEC_GFM_EXT)
 MEC_FOR_K(MEC_GG8_EXT, 1) MEC_FOR_K(MEC_GG8_EXT, 2) MEC_FOR_K(MEC_GG8_EXT, 3) MEC_FOR_K(MEC_GG8_EXT, 4)
 MEC_FOR_W(MEC_FOR_R8, MEC_BM_EXT)
 MEC_FOR_W(MEC_FOR_R8, MEC_GBM_EXT)
@@ -302,6 +302,12 @@ uint32_t ceil_even(double x) { return 2u * uint32_t(std::ceil(x / 2.0)); }
 uint32_t clampw(uint32_t w, uint32_t lo, uint32_t hi) { return std::min(hi, std::max(lo, w)); }
 }  // namespace
 
+uint32_t gf8_stagger(int rows, bool in_place, bool dense, bool accumulate) {
+    const int64_t e = knob(kKnobStagger);  // experiments (mec_set_knob)
+    if (e != kKnobUnset) return uint32_t(std::clamp<int64_t>(e, 0, 64));
+    return in_place && dense && !accumulate && rows == 4 ? 4u : 0u;
+}
+
 uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accumulate) {
     // read-modify-write of the outputs (delta updates, K = 1): each wave
     // also loads its R outputs; R = 2 / 3 / 4 want 16-18 / 12 / 10-12
@@ -402,6 +408,12 @@ constexpr std::array<Gf8MgFn, sizeof...(I)> make_gfm_table(std::index_sequence<I
 }
 const auto kGfmTable = make_gfm_table(std::make_index_sequence<kMaxK * 2>{});
 
+template <size_t... I>
+constexpr std::array<Gf8MgFn, sizeof...(I)> make_gfm8_table(std::index_sequence<I...>) {
+    return {{&run_gf8_mg<int(I) + kMg8MinK, 8>...}};
+}
+const auto kGfm8Table = make_gfm8_table(std::make_index_sequence<kMg8MaxK - kMg8MinK + 1>{});
+
 using BmFn = hipError_t (*)(const BmLaunch &, hipStream_t);
 
 template <size_t... I>
@@ -489,11 +501,16 @@ hipError_t launch_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
     if (L.k < 1 || L.k > kMaxK || L.rows <= kMaxRows || L.rows > kMaxSrc || !L.tabs || L.len % 16) return hipErrorInvalidValue;
     if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
     if (L.len / 16 > uint64_t(UINT32_MAX)) return hipErrorInvalidValue;
-    return kGfmTable[size_t(L.k - 1) * 2 + size_t(gf8_mg_rows(L.rows) - 3)](L, stream);
+    if (L.group_rows == 8) {
+        if (L.k < kMg8MinK || L.k > kMg8MaxK) return hipErrorInvalidValue;
+        return kGfm8Table[size_t(L.k - kMg8MinK)](L, stream);
+    }
+    if (L.group_rows != 3 && L.group_rows != 4) return hipErrorInvalidValue;
+    return kGfmTable[size_t(L.k - 1) * 2 + size_t(L.group_rows - 3)](L, stream);
 }
 
-void gf8_mg_tables(const uint8_t *coef, int rows, int k, std::vector<uint32_t> &out) {
-    const int R = gf8_mg_rows(rows), groups = (rows + R - 1) / R;
+void gf8_mg_tables(const uint8_t *coef, int rows, int k, int R, std::vector<uint32_t> &out) {
+    const int groups = (rows + R - 1) / R;
     out.assign(size_t(groups) * R * k * 8, 0u);
     for (int r = 0; r < rows; ++r)
         for (int j = 0; j < k; ++j) {

@@ -108,29 +108,41 @@ struct GatherLaunch {
 };
 
 // Host side of a multi-group launch: rows (> kMaxRows) outputs at dst_off,
-// coef[r * k + j]; the permute tables in device memory (tabs, from
-// gf8_mg_tables for the same coef and R = gf8_mg_rows(rows)).
+// coef[r * k + j], in groups of group_rows (gf8_mg_rows); the permute tables
+// in device memory (tabs, from gf8_mg_tables for the same coef and
+// group_rows).
 struct Gf8MgLaunch {
     const uint8_t *src;
     uint8_t *dst;
     int64_t src_stripe_stride, dst_stripe_stride;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[kMaxSrc];
-    int k, rows;
+    int k, rows, group_rows;
     uint64_t len;
     uint32_t n_stripes;
     bool accumulate, vand;
     const uint32_t *tabs;
 };
-// Rows per group: 3 or 4, whichever pads fewer rows (5 -> 3+2, 6 -> 3+3,
-// 7 -> 4+3, 8 -> 4+4, 9 -> 3+3+3).
-inline int gf8_mg_rows(int rows) {
+// 8-row groups are instantiated for these source counts.
+constexpr int kMg8MinK = 12, kMg8MaxK = 20;
+// Rows per group.  Groups of 8 when the rows split into whole groups of 8
+// and the sources are many: each source's bit fields are extracted once per
+// group, so 8-row groups halve that work against two groups of 4, at 160-230
+// VGPRs instead of 130-150 (one wave less per SIMD).  Measured at 64 KiB
+// chunks (tools/wide_r8_probe.hip, profiles/r04/probes/wide_r8_probe_box*.log,
+// groups of 4 -> 8): RS(16,8) 63.5 -> 69.0 %, RS(20,8) 61.9 -> 62.4, dense
+// ISA-L Cauchy(12,8) 63.2 -> 65.2, Cauchy(20,8) 55.3 -> 56.4, Cauchy(16,8)
+// and RS(24,8) even; Vandermonde K = 10 and 12 (whose first group skips row
+// 0's products) lose 0.5-3 points.  Otherwise 3 or 4, whichever pads fewer
+// rows (5 -> 3+2, 6 -> 3+3, 7 -> 4+3, 8 -> 4+4, 9 -> 3+3+3).
+inline int gf8_mg_rows(int rows, int k, bool vand) {
+    if (rows % 8 == 0 && k <= kMg8MaxK && (k >= 16 || (!vand && k >= kMg8MinK))) return 8;
     const int g4 = (rows + 3) / 4, g3 = (rows + 2) / 3;
     return g4 * 4 - rows <= g3 * 3 - rows ? 4 : 3;
 }
 // The permute-table image for coef (rows x k) at R rows per group: groups x
 // R x k x 8 dwords, padding rows zero.
-void gf8_mg_tables(const uint8_t *coef, int rows, int k, std::vector<uint32_t> &out);
+void gf8_mg_tables(const uint8_t *coef, int rows, int k, int R, std::vector<uint32_t> &out);
 
 hipError_t launch_gf8(const Gf8Launch &L, hipStream_t stream);
 hipError_t launch_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream);

@@ -38,7 +38,8 @@ struct Knobs {
             Knob k;
         } kPlain[] = {{"MEC_WINDOWS", kKnobWindows}, {"MEC_BLOCK", kKnobBlock},   {"MEC_GBLOCK", kKnobGblock},
                       {"MEC_GWPC", kKnobGwpc},       {"MEC_BM_VW", kKnobBmVw},     {"MEC_WPC", kKnobWpc},
-                      {"MEC_COPY_THREADS", kKnobCopyThreads}, {"MEC_WIDE", kKnobWide}};
+                      {"MEC_COPY_THREADS", kKnobCopyThreads}, {"MEC_WIDE", kKnobWide},
+                      {"MEC_MG_ROWS", kKnobMgRows},  {"MEC_STAGGER", kKnobStagger}};
         for (const auto &p : kPlain)
             if (!std::strcmp(name, p.name)) {
                 put(p.k, num);

@@ -47,10 +47,11 @@ void bit_block(const Field &f, unsigned e, uint32_t w, uint8_t *mask, size_t mst
 
 // The device copy of coef's multi-group permute tables (gf8_mg_kernel),
 // uploaded at first use and kept for the context's lifetime.
-int mg_tables(mec_ctx *c, const Mat &coef, size_t rows, size_t ns, const uint32_t *&out) {
+int mg_tables(mec_ctx *c, const Mat &coef, size_t rows, size_t ns, int R, const uint32_t *&out) {
     std::string key(reinterpret_cast<const char *>(coef.data()), rows * ns);
     key += char(rows);
     key += char(ns);
+    key += char(R);
     std::lock_guard<std::mutex> g(c->mg_mu);
     auto it = c->mg_tabs.find(key);
     if (it != c->mg_tabs.end()) {
@@ -58,7 +59,7 @@ int mg_tables(mec_ctx *c, const Mat &coef, size_t rows, size_t ns, const uint32_
         return MEC_OK;
     }
     std::vector<uint32_t> img;
-    mec::gf8_mg_tables(coef.data(), int(rows), int(ns), img);
+    mec::gf8_mg_tables(coef.data(), int(rows), int(ns), R, img);
     uint32_t *d = nullptr;
     DeviceGuard dg(c->device);
     HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), img.size() * sizeof(uint32_t)));
@@ -103,7 +104,11 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
         for (size_t j = 0; j < ns && vand; ++j) vand = coef[j] == 1;
         for (size_t r = 0; r < nd && vand; ++r) vand = coef[r * ns] == 1;
         L.vand = vand;
-        int rc = mg_tables(c, coef, nd, ns, L.tabs);
+        L.group_rows = mec::gf8_mg_rows(int(nd), int(ns), vand);
+        const int64_t kr = mec::detail::knob(mec::detail::kKnobMgRows);  // experiments (mec_set_knob)
+        if (kr == 3 || kr == 4 || (kr == 8 && ns >= size_t(mec::kMg8MinK) && ns <= size_t(mec::kMg8MaxK)))
+            L.group_rows = int(kr);
+        int rc = mg_tables(c, coef, nd, ns, L.group_rows, L.tabs);
         if (rc != MEC_OK) return rc;
         HIP_TRY(mec::launch_gf8_mg(L, stream));
         return MEC_OK;

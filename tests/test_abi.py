@@ -158,7 +158,7 @@ def test_knobs_through_the_api_not_the_environment():
     import memec_amd
     for name, value in (("MEC_WPC", "12"), ("MEC_SGROUP", "0"), ("MEC_SGROUP", "16:8"), ("MEC_BLOCK", "256"),
                         ("MEC_BM_VW", "2"), ("MEC_GBLOCK", "64"), ("MEC_GWPC", "0"), ("MEC_WINDOWS", "2"),
-                        ("MEC_COPY_THREADS", "4")):
+                        ("MEC_COPY_THREADS", "4"), ("MEC_WIDE", "0"), ("MEC_MG_ROWS", "8"), ("MEC_STAGGER", "0")):
         memec_amd.set_knob(name, value)
         memec_amd.set_knob(name, None)
     with pytest.raises(MecError):

@@ -121,6 +121,37 @@ def test_wide_decode_vs_oracle(fam):
     c.close()
 
 
+@pytest.mark.parametrize("rows", ["3", "4", "8", None])
+@pytest.mark.parametrize("fam", ["rs", "isal_cauchy"])
+def test_wide_group_rows_forced(fam, rows, knobs):
+    """8 outputs coded in groups of 3, 4 or 8 rows (MEC_MG_ROWS; the rule
+    picks 8 for RS(16,8) and the dense ISA-L Cauchy(12,8)): same bytes,
+    encode and in-place decode of 8 erasures, plus an accumulating update."""
+    knobs("MEC_MG_ROWS", rows)
+    for k, m, cs, n in [(16, 8, 4096, 3), (12, 8, 2048, 3), (20, 8, 1024, 2), (24, 8, 1024, 2), (12, 16, 512, 2)]:
+        data = O.fill(n * k * cs, 60 + k + m).reshape(n, k, cs)
+        want = np.stack([np.stack(O.encode(fam, k, m, [data[s, j].copy() for j in range(k)], cs)) for s in range(n)])
+        c = Codec(fam, k, m, cs)
+        st = torch.zeros(n, k + m, cs, dtype=torch.uint8, device=DEV)
+        st[:, :k] = dev(data)
+        c.encode(st[:, :k], st[:, k:])
+        assert np.array_equal(host(st[:, k:]), want), (fam, rows, k, m)
+        pat = list(range(0, k + m, 3))[:m]
+        t = st.clone()
+        t[:, pat] = 0
+        c.decode(t, sum(1 << i for i in range(k + m) if i not in pat))
+        torch.cuda.synchronize()
+        assert torch.equal(t, st), (fam, rows, k, m, pat)
+        delta = O.fill(n * cs, 61 + k).reshape(n, cs)
+        d2 = data.copy()
+        d2[:, 1] ^= delta
+        par = st[:, k:].clone()
+        c.encode_update(1, dev(delta), par)
+        want2 = np.stack([np.stack(O.encode(fam, k, m, [d2[s, j].copy() for j in range(k)], cs)) for s in range(n)])
+        assert np.array_equal(host(par), want2), (fam, rows, k, m, "update")
+        c.close()
+
+
 @pytest.mark.parametrize("fam", ["rs", "cauchy", "isal_rs"])
 def test_wide_roundtrip_every_pattern_small(fam):
     """RS(3,6)-sized code: every erasure pattern of 5 and 6 chunks."""

@@ -10,7 +10,7 @@
 set -u
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-OUT=gpurun_out
+OUT=gpurun_out/${TAG:-r01}
 mkdir -p "$OUT"
 TAG=${TAG:-r01}
 
@@ -22,6 +22,9 @@ run() {  # name seconds cmd...
     local rc=$?
     echo "=== $name rc=$rc" | tee -a "$OUT/session.log"
     tail -n 25 "$OUT/$name.log"
+    if grep -q "illegal memory access\|Memory access fault\|hipErrorIllegalAddress\|HSA_STATUS_ERROR" "$OUT/$name.log"; then
+        echo "stopping: $name hit a GPU fault"; exit 3
+    fi
     case $rc in
         0|1|5) return 0 ;;   # pass / test failures / no tests: not a GPU fault
         *) echo "stopping: $name rc=$rc"; exit $rc ;;
@@ -31,6 +34,12 @@ run() {  # name seconds cmd...
 for step in "$@"; do
     case $step in
         tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+        testsel)  # TESTSEL=group,group,...; a group is file[::test]+file...; one process per group
+            i=0
+            for grp in $(echo "$TESTSEL" | tr ',' ' '); do
+                i=$((i + 1))
+                run "pytest_sel_$i" 600 python -u -m pytest $(echo "$grp" | tr '+' ' ') -m gpu -x -v --timeout 120 --timeout-method thread
+            done ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py ;;
         benchdec) run bench_rs_dec 400 python bench.py --config rs_dec ;;
@@ -69,6 +78,16 @@ for step in "$@"; do
         server) run server_pattern 900 bash tools/server_pattern.sh ;;
         stagger) run stagger_probe 300 tools/stagger_probe 4096 3 ;;
         wider8) run wide_r8_probe 300 tools/wide_r8_probe 16384 3 ;;
+        staggerab)  # the store stagger rule against MEC_STAGGER=0, decode configs, interleaved
+            for r in 1 2; do
+                for c in ${STAGGER_CONFIGS:-rs_dec rs_dec_mixed}; do
+                    for st in rule 0 6; do
+                        if [ $st = rule ]; then e=MEC_STAGGER_UNSET=1; else e=MEC_STAGGER=$st; fi
+                        run "stagger_${c}_${st}_$r" 200 env $e python bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 10
+                        grep -h '^{' "$OUT/stagger_${c}_${st}_$r.log" | sed "s/^{/{\"stagger\": \"$st\", \"round\": $r, /" >> "$OUT/staggerab.jsonl"
+                    done
+                done
+            done ;;
         mixed)
             for w in 1 4 16; do
                 run "mixed_w$w" 120 tools/mixed_ab 1024 $w 3 32

@@ -66,7 +66,7 @@ void shape(int family, const char *name, uint32_t n, int rounds) {
     std::vector<uint8_t> coef(size_t(M) * K);
     for (int i = 0; i < M * K; ++i) coef[size_t(i)] = uint8_t(A[size_t(off + i)]);
     std::vector<uint32_t> img;
-    gf8_mg_tables(coef.data(), M, K, img);
+    gf8_mg_tables(coef.data(), M, K, 8, img);  // M % 8 == 0: the same image at R = 4
     uint32_t *tabs = nullptr;
     CK(hipMalloc((void **)&tabs, img.size() * 4));
     CK(hipMemcpy(tabs, img.data(), img.size() * 4, hipMemcpyHostToDevice));
@@ -92,6 +92,7 @@ void shape(int family, const char *name, uint32_t n, int rounds) {
     for (int rd = 0; rd < rounds; ++rd)
         for (int R : {4, 8}) {
             L.dst = R == 8 ? p8 : p4;
+            L.group_rows = R;
             const float ms = time_arm<K>(R, L);
             printf("{\"round\": %d, \"shape\": \"%s\", \"R\": %d, \"ms\": %.4f, \"frac\": %.4f}\n", rd, name, R, ms,
                    alg / (ms * 1e-3) / 8e12);
@@ -116,5 +117,8 @@ int main(int argc, char **argv) {
     shape<12>(MEC_ISAL_RS, "ISA-L RS(12,8)@64KiB encode", n, rounds);
     shape<12>(MEC_ISAL_CAUCHY, "ISA-L Cauchy(12,8)@64KiB encode", n, rounds);
     shape<10>(MEC_RS_VANDERMONDE, "RS(10,8)@64KiB encode", n, rounds);
+    shape<16>(MEC_ISAL_CAUCHY, "ISA-L Cauchy(16,8)@64KiB encode", n, rounds);
+    shape<20>(MEC_RS_VANDERMONDE, "RS(20,8)@64KiB encode", n / 2, rounds);
+    shape<20>(MEC_ISAL_CAUCHY, "ISA-L Cauchy(20,8)@64KiB encode", n / 2, rounds);
     return 0;
 }
