@@ -78,6 +78,16 @@ for step in "$@"; do
         server) run server_pattern 900 bash tools/server_pattern.sh ;;
         stagger) run stagger_probe 300 tools/stagger_probe 4096 3 ;;
         wider8) run wide_r8_probe 300 tools/wide_r8_probe 16384 3 ;;
+        staggerpmc)  # EA counters per stagger_probe arm (tools/stagger_pmc.py)
+            arms=${STAGGER_ARMS:-split_enc,split_twin_cap12,split_dense_cap12,inplace_dec,inplace_dec_sleep32,inplace_twin,inplace_vand}
+            run stagger_plain 200 tools/stagger_probe 2048 1 "$arms"
+            run stagger_pmc_a 200 timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_LEVEL_sum \
+                TCC_EA0_WRREQ_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/stagger_pmc_a" -o run -- tools/stagger_probe 2048 1 "$arms"
+            run stagger_pmc_b 200 timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_WRREQ_STALL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum \
+                TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/stagger_pmc_b" -o run -- tools/stagger_probe 2048 1 "$arms"
+            run stagger_pmc_c 200 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU \
+                SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/stagger_pmc_c" -o run -- tools/stagger_probe 2048 1 "$arms"
+            python3 tools/stagger_pmc.py "$arms" "$OUT/stagger_pmc_a" "$OUT/stagger_pmc_b" "$OUT/stagger_pmc_c" > "$OUT/stagger_pmc.jsonl" ;;
         staggerab)  # the store stagger rule against MEC_STAGGER=0, decode configs, interleaved
             for r in 1 2; do
                 for c in ${STAGGER_CONFIGS:-rs_dec rs_dec_mixed}; do

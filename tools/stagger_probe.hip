@@ -13,11 +13,16 @@
 // Timing only (outputs are not checked: any dense 4 x 10 matrix costs the
 // same); each arm best of 5 launches, arms interleaved over `rounds`.
 //
-//   stagger_probe [stripes=4096] [rounds=2]
+//   stagger_probe [stripes=4096] [rounds=2] [arm,arm,...]
+// (the arm list selects and orders arms: under rocprofv3 --pmc every arm is
+// 6 dispatches of probe_kernel, one untimed then 5 timed, in list order;
+// tools/stagger_pmc.py sums the counters per arm)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <string>
 #include <vector>
 
 #include "gf8_kernel.hpp"
@@ -136,6 +141,27 @@ int main(int argc, char **argv) {
         {"split_twin", false, kGf8Xor, 0, false},             {"split_twin_cap12", false, kGf8Xor, 0, false, 12},
         {"split_dense", false, kGf8Dense, 0, false},          {"split_dense_cap12", false, kGf8Dense, 0, false, 12},
     };
+    if (argc > 3) {
+        std::vector<Arm> pick;
+        std::string list = argv[3];
+        size_t at = 0;
+        while (at <= list.size()) {
+            const size_t e = std::min(list.find(',', at), list.size());
+            const std::string name = list.substr(at, e - at);
+            bool found = false;
+            for (const Arm &a : arms)
+                if (name == a.name) {
+                    pick.push_back(a);
+                    found = true;
+                }
+            if (!found) {
+                fprintf(stderr, "unknown arm %s\n", name.c_str());
+                return 2;
+            }
+            at = e + 1;
+        }
+        arms = pick;
+    }
     const double alg = double(n) * (K + R) * CS;
     for (int rd = 0; rd < rounds; ++rd) {
         for (const Arm &a : arms) {
