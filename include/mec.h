@@ -117,7 +117,7 @@ typedef struct {
     uint32_t queue_slots;        /* slots actually running (mec_set_host_queue may grant fewer) */
     uint32_t queue_parts;        /* workgroups per slot (one per 16 KiB of chunk, at most 64) */
     uint32_t queue_broken;       /* 1: a call timed out and the queue stopped for good */
-    uint32_t pad0;
+    uint32_t queue_devslot;      /* 1: slot descriptors in device memory, written through the BAR */
     uint64_t queue_timeouts;     /* calls that hit MEC_QUEUE_TIMEOUT_MS */
 } mec_stats;
 

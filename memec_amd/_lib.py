@@ -42,7 +42,7 @@ class MecStats(ctypes.Structure):
                 ("cached_plans", ctypes.c_uint64), ("zero_copy_calls", ctypes.c_uint64),
                 ("staged_calls", ctypes.c_uint64), ("queue_calls", ctypes.c_uint64),
                 ("queue_launches", ctypes.c_uint64), ("queue_slots", ctypes.c_uint32),
-                ("queue_parts", ctypes.c_uint32), ("queue_broken", ctypes.c_uint32), ("pad0", ctypes.c_uint32),
+                ("queue_parts", ctypes.c_uint32), ("queue_broken", ctypes.c_uint32), ("queue_devslot", ctypes.c_uint32),
                 ("queue_timeouts", ctypes.c_uint64)]
 
 

@@ -211,7 +211,7 @@ class Codec:
                 "cached_plans": st.cached_plans, "zero_copy_calls": st.zero_copy_calls,
                 "staged_calls": st.staged_calls, "queue_calls": st.queue_calls,
                 "queue_launches": st.queue_launches, "queue_slots": st.queue_slots,
-                "queue_parts": st.queue_parts, "queue_broken": bool(st.queue_broken),
+                "queue_parts": st.queue_parts, "queue_broken": bool(st.queue_broken), "queue_devslot": bool(st.queue_devslot),
                 "queue_timeouts": st.queue_timeouts}
 
 

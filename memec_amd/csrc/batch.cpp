@@ -934,6 +934,7 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
     out->queue_slots = c->hq ? c->hq->slots : 0;
     out->queue_parts = c->hq ? c->hq->parts : 0;
     out->queue_broken = c->hq && c->hq->broken.load() ? 1u : 0u;
+    out->queue_devslot = c->hq && c->hq->dslot ? 1u : 0u;
     out->queue_timeouts = c->hq ? c->hq->timeouts.load() : 0;
     {
         std::lock_guard<std::mutex> pk(c->plan_mu);
@@ -952,6 +953,7 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
         out->queue_slots += t.queue_slots;
         out->queue_parts = std::max(out->queue_parts, t.queue_parts);
         out->queue_broken |= t.queue_broken;
+        out->queue_devslot |= t.queue_devslot;
         out->queue_timeouts += t.queue_timeouts;
     }
     return MEC_OK;

@@ -112,14 +112,10 @@ constexpr uint32_t kQMaxParts = 64;  // workgroups per slot (one call's chunk sp
 // for the resident grid to leave before it gives up with MEC_EHIP (queue_try)
 constexpr uint64_t kQDrainFactor = 4;
 constexpr uint32_t kQBmRows = kQMaxDst * 8;  // bitmatrix output packet rows (outputs x w <= 8)
-struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
-    // host -> GPU: (number of the posted job << 16) | (sources << 8) |
-    // outputs — the poll that sees a job also sizes its descriptor read
-    uint64_t seq;
-    uint64_t pad0[15];
-    uint64_t done[kQMaxParts];  // GPU -> host: number of the last job each part finished
-    // sources, outputs, chunk bytes, accumulate, w (0: byte-wise GF(2^8);
-    // 1..8: Jerasure bitmatrix over w packets), packet bytes, trace, -
+// A job's descriptor (host -> GPU): sources, outputs, chunk bytes,
+// accumulate, w (0: byte-wise GF(2^8); 1..8: Jerasure bitmatrix over w
+// packets), packet bytes, trace, -; then chunk addresses and tables.
+struct QDesc {
     uint32_t hdr[8];
     uint64_t src[kQMaxSrc];  // device addresses of registered chunks (0 = zeros)
     uint64_t dst[kQMaxDst];  // (0 = unwanted output)
@@ -130,16 +126,35 @@ struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
         uint32_t tab_w[kQMaxDst * kQMaxSrc * 5];
         uint32_t mask_w[kQMaxSrc * kQBmRows / 4];  // bitmatrix bytes [source][output*w + l], bit x
     };
+};
+struct alignas(128) QSlot {  // in GPU-mapped coherent host memory
+    // host -> GPU: (number of the posted job << 16) | (sources << 8) |
+    // outputs — the poll that sees a job also sizes its descriptor read
+    // (host-memory slots; device-memory slots carry it in QDevSlot)
+    uint64_t seq;
+    uint64_t pad0[15];
+    uint64_t done[kQMaxParts];  // GPU -> host: number of the last job each part finished
+    QDesc d;                    // the descriptor (host-memory slots; the host's staging copy otherwise)
     // GPU -> host when hdr[6] (trace) is set: part 0's s_memrealtime when it
     // took the job, after its acquire fence, with the descriptor in LDS,
     // when thread 0's source loads had returned, and with its output stores
     // acknowledged (just before its done store)
     uint64_t trace[5];
 };
+// The host -> GPU half of a slot in device memory (uncached), written by the
+// host through the PCIe BAR: part 0 then polls HBM and reads the
+// descriptor from HBM instead of over PCIe (queue_try, MEC_QUEUE_DEVSLOT).
+struct alignas(256) QDevSlot {
+    uint64_t seq;
+    uint64_t pad0[7];
+    QDesc d;
+};
 // Grid-wide control words, after the slots in the same mapped allocation.
 enum : uint32_t { kQCtlStop = 0, kQCtlExit = 1, kQCtlWords = 2 };
 struct HostQueue {
     QSlot *host = nullptr, *dev = nullptr;
+    QDevSlot *dslot = nullptr;        // device-memory slot halves (large-BAR devices), else null
+    uint64_t *seqno = nullptr;        // per slot: number of the last job posted (host only)
     uint32_t *ctl_host = nullptr, *ctl_dev = nullptr;  // [kQCtlStop] host -> GPU, [kQCtlExit] leader -> grid
     uint64_t *act = nullptr;          // device memory: per-slot time of the last job (s_memrealtime)
     // device memory, per slot: [0, slots) the job part 0 took (`go`, read by

@@ -45,8 +45,10 @@
 // over w packets of chunk/w bytes (cauchycoding.cc:80), whose masks the
 // caller expands from the GF(2^w) coefficients.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <chrono>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -240,8 +242,11 @@ constexpr uint32_t kQHeadWords = 8 + 2 * (kQMaxSrc + kQMaxDst);
 constexpr uint32_t kQDescWords = kQHeadWords + kQMaxDst * kQMaxSrc * 5;  // the tables outsize the masks
 static_assert(kQMaxDst * kQMaxSrc * 5 >= kQMaxSrc * kQBmRows / 4, "descriptor LDS holds the masks");
 static_assert(kQHeadWords % 4 == 0, "16-byte descriptor loads");
+static_assert(offsetof(QDesc, tab_w) == kQHeadWords * 4, "descriptor head layout");
+static_assert(offsetof(QSlot, d) % 16 == 0 && offsetof(QDevSlot, d) % 16 == 0, "16-byte descriptor loads");
+static_assert(sizeof(QDevSlot) % 64 == 0, "device slots on their own cache lines");
 // dwords of a job's descriptor: the head, then its tables / masks
-__device__ __forceinline__ uint32_t desc_words(uint32_t ns, uint32_t nd, bool bitmatrix) {
+__host__ __device__ __forceinline__ uint32_t desc_words(uint32_t ns, uint32_t nd, bool bitmatrix) {
     return kQHeadWords + (bitmatrix ? ns * (kQBmRows / 4) : nd * ns * 5);
 }
 
@@ -254,7 +259,11 @@ __device__ __forceinline__ uint32_t desc_words(uint32_t ns, uint32_t nd, bool bi
 // the other parts leave only after that, having run every job part 0 took
 // — so a job is run by all of a slot's parts or by none (a withdrawn job
 // is never taken, queue_try).
-__global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t *ctl, uint64_t *act, uint64_t *link,
+// The slot's sequence word and descriptor are at seq_base / desc_base +
+// slot * dstride: inside the host-memory QSlot, or in device memory
+// (QDevSlot) that the host writes through the BAR.
+__global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, const uint8_t *seq_base, const uint8_t *desc_base,
+                                                         uint32_t dstride, uint32_t *ctl, uint64_t *act, uint64_t *link,
                                                          uint64_t epoch, uint64_t idle_ticks, uint32_t nthr,
                                                          uint32_t nslots, uint32_t parts, uint32_t bitmatrix) {
     __shared__ u32x4 desc4[kQDescWords / 4];  // the slot's descriptor: hdr, src, dst, tab_w | mask_w
@@ -262,6 +271,8 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
     uint32_t *desc = reinterpret_cast<uint32_t *>(desc4);
     const uint32_t si = blockIdx.x / parts, part = blockIdx.x - si * parts;
     QSlot *s = slots + si;
+    const uint64_t *seqp = reinterpret_cast<const uint64_t *>(seq_base + size_t(si) * dstride);
+    const u32x4 *sw = reinterpret_cast<const u32x4 *>(desc_base + size_t(si) * dstride);
     uint64_t *go = link + si, *left = link + nslots + si;
     const uint32_t t = threadIdx.x;
     const bool leader = blockIdx.x == 0;
@@ -312,7 +323,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
         } else if (t == 0) {
             uint32_t c = 0;
             for (uint32_t n = 1;; ++n) {  // one PCIe read per poll; control words every 64th
-                const uint64_t q = __hip_atomic_load(&s->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint64_t q = __hip_atomic_load(seqp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 if ((q >> 16) > last) {  // a withdrawn job moves seq back (queue_try)
                     t_take = __builtin_amdgcn_s_memrealtime();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, once per job
@@ -348,7 +359,6 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, uint32_t
         {  // descriptor: the head, then this job's tables or masks only (its
            // size came with the seq word), 16 bytes per lane, one round trip
             const uint32_t n4 = (desc_words(shape >> 8, shape & 0xffu, bitmatrix != 0) + 3) / 4;
-            const u32x4 *sw = reinterpret_cast<const u32x4 *>(&s->hdr[0]);
             for (uint32_t i = t; i < n4; i += nthr) desc4[i] = __builtin_nontemporal_load(sw + i);
         }
         __syncthreads();
@@ -436,7 +446,13 @@ int queue_launch(mec_ctx *c, HostQueue *q) {
     DeviceGuard dg(c->device);
     __atomic_store_n(q->ctl_host + kQCtlExit, 0u, __ATOMIC_RELEASE);
     ++q->epoch;
-    hipLaunchKernelGGL(queue_kernel, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev, q->ctl_dev,
+    const uint8_t *seq_base = q->dslot ? reinterpret_cast<const uint8_t *>(&q->dslot->seq)
+                                       : reinterpret_cast<const uint8_t *>(&q->dev->seq);
+    const uint8_t *desc_base = q->dslot ? reinterpret_cast<const uint8_t *>(&q->dslot->d)
+                                        : reinterpret_cast<const uint8_t *>(&q->dev->d);
+    const uint32_t dstride = q->dslot ? uint32_t(sizeof(QDevSlot)) : uint32_t(sizeof(QSlot));
+    hipLaunchKernelGGL(queue_kernel, dim3(q->slots * q->parts), dim3(q->threads), 0, q->stream, q->dev, seq_base,
+                       desc_base, dstride, q->ctl_dev,
                        q->act, q->link, q->epoch, q->idle_ticks, q->threads, q->slots, q->parts,
                        c->byte_wise() ? 0u : 1u);
     HIP_TRY(hipGetLastError());
@@ -489,8 +505,10 @@ void queue_stop(mec_ctx *c) {
         (void)hipHostFree(q->host);
         (void)hipFree(q->act);
         (void)hipFree(q->link);
+        if (q->dslot) (void)hipFree(q->dslot);
     }
     delete[] q->busy;
+    delete[] q->seqno;
     delete q;
 }
 
@@ -543,6 +561,24 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     }
     q->host = static_cast<QSlot *>(h);
     q->dev = static_cast<QSlot *>(d);
+    q->seqno = new uint64_t[slots]();
+    // device-memory slot halves when the host can store to device memory
+    // (large BAR): uncached, so part 0's polls and descriptor reads never
+    // meet a stale L2 line; MEC_QUEUE_DEVSLOT=0 keeps them in host memory
+    {
+        int large_bar = 0;
+        if (hipDeviceGetAttribute(&large_bar, hipDeviceAttributeIsLargeBar, c->device) != hipSuccess) large_bar = 0;
+        if (large_bar && env_u64("MEC_QUEUE_DEVSLOT", 1) != 0) {
+            void *ds = nullptr;
+            if (hipExtMallocWithFlags(&ds, sizeof(QDevSlot) * slots, hipDeviceMallocUncached) == hipSuccess) {
+                if (hipMemset(ds, 0, sizeof(QDevSlot) * slots) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
+                    q->dslot = static_cast<QDevSlot *>(ds);
+                else
+                    (void)hipFree(ds);
+            }
+            (void)hipGetLastError();  // a refused allocation leaves host-memory slots
+        }
+    }
     q->ctl_host = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(h) + sizeof(QSlot) * slots);
     q->ctl_dev = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d) + sizeof(QSlot) * slots);
     q->busy = new std::atomic<bool>[slots];
@@ -560,7 +596,9 @@ int queue_start(mec_ctx *c, uint32_t slots) {
         (void)hipHostFree(h);
         (void)hipFree(q->act);
         (void)hipFree(q->link);
+        if (q->dslot) (void)hipFree(q->dslot);
         delete[] q->busy;
+        delete[] q->seqno;
         return hip_fail(e, "queue stream");
     }
     {
@@ -571,7 +609,9 @@ int queue_start(mec_ctx *c, uint32_t slots) {
             (void)hipHostFree(h);
             (void)hipFree(q->act);
             (void)hipFree(q->link);
+            if (q->dslot) (void)hipFree(q->dslot);
             delete[] q->busy;
+            delete[] q->seqno;
             return rc;
         }
     }
@@ -598,29 +638,48 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     hint = i;
     q->inflight.fetch_add(1, std::memory_order_relaxed);
     QSlot *s = q->host + i;
-    s->hdr[0] = uint32_t(ns);
-    s->hdr[1] = uint32_t(nd);
-    s->hdr[2] = c->cs;
-    s->hdr[3] = accumulate ? 1u : 0u;
-    s->hdr[4] = c->byte_wise() ? 0u : c->w;
-    s->hdr[5] = c->byte_wise() ? c->cs : c->packet;
+    QDesc &d = s->d;  // built in host memory (the device copy follows, below)
+    d.hdr[0] = uint32_t(ns);
+    d.hdr[1] = uint32_t(nd);
+    d.hdr[2] = c->cs;
+    d.hdr[3] = accumulate ? 1u : 0u;
+    d.hdr[4] = c->byte_wise() ? 0u : c->w;
+    d.hdr[5] = c->byte_wise() ? c->cs : c->packet;
     const bool traced = q->trace.load(std::memory_order_relaxed);
-    s->hdr[6] = traced ? 1u : 0u;
-    for (size_t j = 0; j < ns; ++j) s->src[j] = addrs[j];
-    for (size_t r = 0; r < nd; ++r) s->dst[r] = addrs[ns + r];
+    d.hdr[6] = traced ? 1u : 0u;
+    for (size_t j = 0; j < ns; ++j) d.src[j] = addrs[j];
+    for (size_t r = 0; r < nd; ++r) d.dst[r] = addrs[ns + r];
     if (c->byte_wise()) {  // the v_perm tables, [output][source] (a table per GF(2^8) value)
-        for (size_t b = 0; b < nd * ns; ++b) std::memcpy(&s->tab_w[b * 5], &gf8_coef_table()[coef[b]], sizeof(Gf8Coef));
+        for (size_t b = 0; b < nd * ns; ++b) std::memcpy(&d.tab_w[b * 5], &gf8_coef_table()[coef[b]], sizeof(Gf8Coef));
     } else {  // GF(2^w) coefficients -> bitmatrix rows (jerasure_matrix_to_bitmatrix)
         const Field &f = Field::get(int(c->w));
         uint8_t mk[kQMaxSrc][kQBmRows] = {};
         for (size_t r = 0; r < nd; ++r)
             for (size_t j = 0; j < ns; ++j) bit_block(f, coef[r * ns + j], c->w, &mk[j][r * c->w], 1);
-        std::memcpy(s->mask_w, mk, sizeof(mk));
+        std::memcpy(d.mask_w, mk, sizeof(mk));
     }
-    const uint64_t seq = (__atomic_load_n(&s->seq, __ATOMIC_RELAXED) >> 16) + 1;
+    const uint64_t seq = q->seqno[i] + 1;
+    q->seqno[i] = seq;
     const uint64_t t_post = traced ? mono_ns() : 0;
     // publishes the descriptor; the word carries its shape (sources, outputs)
-    __atomic_store_n(&s->seq, seq << 16 | uint64_t(ns) << 8 | uint64_t(nd), __ATOMIC_RELEASE);
+    const uint64_t word = seq << 16 | uint64_t(ns) << 8 | uint64_t(nd);
+    if (q->dslot) {
+        // through the BAR: the job's prefix of the descriptor in 16-byte
+        // streaming stores, a store fence (the BAR mapping may combine and
+        // reorder them), then the sequence word and another fence so it
+        // leaves the write-combining buffer now; PCIe keeps posted writes in
+        // order, so the GPU that sees the word sees the descriptor
+        QDevSlot *ds = q->dslot + i;
+        const uint32_t n16 = (desc_words(uint32_t(ns), uint32_t(nd), !c->byte_wise()) + 3) / 4;
+        const __m128i *from = reinterpret_cast<const __m128i *>(&d);
+        __m128i *to = reinterpret_cast<__m128i *>(&ds->d);
+        for (uint32_t k = 0; k < n16; ++k) _mm_stream_si128(to + k, _mm_load_si128(from + k));
+        _mm_sfence();
+        _mm_stream_si64(reinterpret_cast<long long *>(&ds->seq), static_cast<long long>(word));
+        _mm_sfence();
+    } else {
+        __atomic_store_n(&s->seq, word, __ATOMIC_RELEASE);
+    }
     // wait for the workgroup; relaunch the grid if it idled out meanwhile
     rc = MEC_OK;
     bool taken = true;
@@ -647,7 +706,13 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
                 // may still be written; an accumulate job must not be run
                 // again on top of the parts that applied it).
                 if (dt > std::chrono::milliseconds(q->timeout_ms)) q->timeouts++;
-                __atomic_store_n(&s->seq, (seq - 1) << 16, __ATOMIC_SEQ_CST);
+                q->seqno[i] = seq - 1;
+                if (q->dslot) {
+                    _mm_stream_si64(reinterpret_cast<long long *>(&q->dslot[i].seq), static_cast<long long>((seq - 1) << 16));
+                    _mm_sfence();
+                } else {
+                    __atomic_store_n(&s->seq, (seq - 1) << 16, __ATOMIC_SEQ_CST);
+                }
                 q->broken.store(true);
                 __atomic_store_n(q->ctl_host + kQCtlStop, 1u, __ATOMIC_RELEASE);
                 const Drain dr = queue_drained(

@@ -80,6 +80,27 @@ def test_queue_encode_decode_update(fam, k, m, cs):
     _encode_decode_update(fam, k, m, cs)
 
 
+@pytest.mark.parametrize("devslot", ["0", "1"])
+@pytest.mark.parametrize("fam", FAMILIES)
+def test_queue_slot_placement(fam, devslot, qenv):
+    """Slot descriptors in device memory written through the BAR (the
+    default on large-BAR devices) and in host memory (MEC_QUEUE_DEVSLOT=0):
+    same results, single- and multi-part slots, and the placement is
+    reported."""
+    qenv(MEC_QUEUE_DEVSLOT=devslot, MEC_QUEUE_MAX_CHUNK=128 << 10)
+    for k, m, cs, parts in [(8, 2, 4096, 1), (10, 4, 65536, 4)]:
+        _encode_decode_update(fam, k, m, cs, parts=parts)
+    c = Codec(fam, 4, 2, 4096)
+    try:
+        c.set_host_queue(2)
+        if devslot == "0":
+            assert not c.stats()["queue_devslot"]
+        elif not c.stats()["queue_devslot"]:
+            pytest.skip("no large BAR: host-memory slots only")
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("k,m,cs", [(4, 2, 4100), (3, 1, 24), (12, 4, 16376), (6, 3, 4104)])
 def test_queue_cauchy_packet_tails(k, m, cs):
     """Bitmatrix packets that are not whole 8-byte units: w=4 / 1025 B,

@@ -78,6 +78,7 @@ for step in "$@"; do
         server) run server_pattern 900 bash tools/server_pattern.sh ;;
         stagger) run stagger_probe 300 tools/stagger_probe 4096 3 ;;
         wider8) run wide_r8_probe 300 tools/wide_r8_probe 16384 3 ;;
+        bar) run bar_probe 120 tools/bar_probe 2000 ;;
         staggerpmc)  # EA counters per stagger_probe arm (tools/stagger_pmc.py)
             arms=${STAGGER_ARMS:-split_enc,split_twin_cap12,split_dense_cap12,inplace_dec,inplace_dec_sleep32,inplace_twin,inplace_vand}
             run stagger_plain 200 tools/stagger_probe 2048 1 "$arms"
