@@ -285,8 +285,12 @@ int mec_set_coalescing(mec_ctx *ctx, uint32_t max_batch);
 
 /* Device-side submission queue for single-stripe host calls (queue.hip).
  * slots > 0 starts a resident kernel with `parts` workgroups per slot (one
- * per 16 KiB of chunk, at most 64; MEC_QUEUE_PARTS overrides), polling
- * GPU-mapped host memory; mec_encode_host / mec_decode_host /
+ * per 16 KiB of chunk, at most 64; MEC_QUEUE_PARTS overrides).  Each
+ * slot's sequence word and descriptor live in device memory that the host
+ * writes through the PCIe BAR when the device has a large BAR
+ * (mec_stats.queue_devslot = 1; MEC_QUEUE_DEVSLOT=0 keeps them in
+ * GPU-mapped host memory), its completion words in host memory;
+ * mec_encode_host / mec_decode_host /
  * mec_encode_update_host calls of every family (RS and ISA-L byte-wise,
  * Jerasure Cauchy-RS as bitmatrix jobs) with chunks of at most
  * MEC_QUEUE_MAX_CHUNK bytes (default 1 MiB) are then posted to a free slot instead of
