@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 PMC passes into profiles/pmc_<config>.json.
 
-Input: gpurun_out/pmc_fetch_<cfg>/run_counter_collection.csv (FETCH_SIZE
-pass) and gpurun_out/pmc_write_<cfg>/run_counter_collection.csv (WRITE_SIZE
-pass), produced by tools/gpu_session.sh pmc.  Corrections per
+Input: gpurun_out/<TAG>/pmc_fetch_<cfg>/run_counter_collection.csv
+(FETCH_SIZE pass) and gpurun_out/<TAG>/pmc_write_<cfg>/run_counter_collection.csv
+(WRITE_SIZE pass), produced by TAG=<TAG> tools/gpu_session.sh pmc
+(PMC_DIR overrides the directory).  Corrections per
 MI355X_MICROARCH.md §HBM: counters are in KiB; on gfx950 FETCH_SIZE reads
 exactly half of a wide coalesced streaming read, so read bytes =
 2 * FETCH_SIZE * 1024; WRITE_SIZE is exact for 16-B-per-lane stores.
@@ -27,7 +28,7 @@ def per_launch(path, counter):
             name = row["Kernel_Name"]
             if row["Counter_Name"] != counter:
                 continue
-            if "gf8_kernel" in name or "bm_kernel" in name:
+            if "gf8_kernel" in name or "gf8_mg_kernel" in name or "bm_kernel" in name:
                 by_name.setdefault(name, []).append(float(row["Counter_Value"]))
     if not by_name:
         return None, 0, []
@@ -40,7 +41,10 @@ def main(cfgs, out_dir, tag):
     sys.path.insert(0, ROOT)
     from bench import CONFIGS
     for cfg in cfgs:
-        base = os.path.join(ROOT, "gpurun_out")
+        # tools/gpu_session.sh writes under gpurun_out/<TAG>/ (older runs: gpurun_out/)
+        base = os.environ.get("PMC_DIR") or os.path.join(ROOT, "gpurun_out", tag)
+        if not os.path.isdir(base):
+            base = os.path.join(ROOT, "gpurun_out")
         fpath = os.path.join(base, "pmc_fetch_%s" % cfg, "run_counter_collection.csv")
         wpath = os.path.join(base, "pmc_write_%s" % cfg, "run_counter_collection.csv")
         if not (os.path.exists(fpath) and os.path.exists(wpath)):
