@@ -13,6 +13,7 @@ The tail kernels never run for these sizes; only the main coding kernel
 """
 import csv
 import json
+import re
 import os
 import sys
 
@@ -27,6 +28,9 @@ def per_launch(path, counter):
         for row in csv.DictReader(f):
             name = row["Kernel_Name"]
             if row["Counter_Name"] != counter:
+                continue
+            # the coding kernels, not bench.py's XOR twin (gf8_kernel S = 2, kGf8Xor)
+            if re.search(r"gf8_kernel<\d+, \d+, (true|false), 2,", name):
                 continue
             if "gf8_kernel" in name or "gf8_mg_kernel" in name or "bm_kernel" in name:
                 by_name.setdefault(name, []).append(float(row["Counter_Value"]))
