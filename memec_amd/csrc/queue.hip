@@ -571,10 +571,14 @@ int queue_start(mec_ctx *c, uint32_t slots) {
         if (large_bar && env_u64("MEC_QUEUE_DEVSLOT", 1) != 0) {
             void *ds = nullptr;
             if (hipExtMallocWithFlags(&ds, sizeof(QDevSlot) * slots, hipDeviceMallocUncached) == hipSuccess) {
-                if (hipMemset(ds, 0, sizeof(QDevSlot) * slots) == hipSuccess && hipDeviceSynchronize() == hipSuccess)
-                    q->dslot = static_cast<QDevSlot *>(ds);
-                else
-                    (void)hipFree(ds);
+                // zeroed through the BAR like every later write (no device-wide
+                // synchronize that would wait for the caller's own launches);
+                // the kernel launch below is a later PCIe write, so it lands after
+                const __m128i z = _mm_setzero_si128();
+                __m128i *w = static_cast<__m128i *>(ds);
+                for (size_t k = 0; k < sizeof(QDevSlot) * slots / 16; ++k) _mm_stream_si128(w + k, z);
+                _mm_sfence();
+                q->dslot = static_cast<QDevSlot *>(ds);
             }
             (void)hipGetLastError();  // a refused allocation leaves host-memory slots
         }
