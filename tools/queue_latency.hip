@@ -106,7 +106,7 @@ static double pct(std::vector<double> v, double p) {
 
 int main(int argc, char **argv) {
     if (argc < 6) {
-        fprintf(stderr, "usage: %s <rs|cauchy|isal_rs> k m chunk calls [registered=1] [nd=1]\n", argv[0]);
+        fprintf(stderr, "usage: %s <rs|cauchy|isal_rs> k m chunk calls [registered=1] [nd=1] [traced=1]\n", argv[0]);
         return 2;
     }
     const int fam = !strcmp(argv[1], "cauchy") ? MEC_CAUCHY_GOOD : !strcmp(argv[1], "isal_rs") ? MEC_ISAL_RS
@@ -115,6 +115,9 @@ int main(int argc, char **argv) {
     const int calls = atoi(argv[5]);
     const bool reg = argc > 6 ? atoi(argv[6]) != 0 : true;
     const uint32_t nd = argc > 7 ? uint32_t(atoi(argv[7])) : 1u;
+    // traced = 0: no device stamps (the trace's own stores delay the done
+    // store); only the host-side total and calls/s are reported
+    const bool traced = argc > 8 ? atoi(argv[8]) != 0 : true;
     CK(hipSetDevice(0));
     int khz = 0;
     CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
@@ -125,7 +128,7 @@ int main(int argc, char **argv) {
     mec_ctx *c = nullptr;
     MK(mec_create(fam, k, m, cs, 0, &c));
     MK(mec_set_host_queue(c, 8));
-    MK(mec_queue_trace_enable(c, 1));
+    MK(mec_queue_trace_enable(c, traced ? 1 : 0));
     const size_t slot = 8 + size_t(cs);  // ChunkPool slot: 8-byte header + data (chunk_pool.cc:22-47)
     const size_t bytes = ((k + m) * slot + 4095) / 4096 * 4096;
     uint8_t *slab = (uint8_t *)aligned_alloc(4096, bytes);
@@ -143,6 +146,10 @@ int main(int argc, char **argv) {
         const uint64_t a = mono_ns();
         MK(mec_encode_host(c, data.data(), par.data()));
         const uint64_t b = mono_ns();
+        if (!traced) {
+            if (it >= warm) seg[8].push_back(double(b - a) * 1e-3);
+            continue;
+        }
         mec_queue_trace tr;
         if (mec_queue_last_trace(&tr) != MEC_OK || it < warm) continue;  // launch path (no trace)
         const double take = double(tr.dev_take) * ns_per_tick - off;
@@ -163,9 +170,9 @@ int main(int argc, char **argv) {
     const double dt = double(mono_ns() - t_start) * 1e-9;
     const char *names[9] = {"pre", "poll", "fence", "desc", "load", "code", "complete", "post", "total"};
     printf("{\"bench\": \"queue_latency\", \"family\": \"%s\", \"k\": %u, \"m\": %u, \"chunk\": %u, \"outputs\": %u, "
-           "\"registered\": %d, \"calls\": %d, \"traced\": %zu, \"calls_per_s\": %.1f, \"clock_window_us\": %.3f",
-           argv[1], k, m, cs, nd, reg ? 1 : 0, calls, seg[8].size(), calls / dt, window * 1e-3);
-    for (int i = 0; i < 9; ++i)
+           "\"registered\": %d, \"calls\": %d, \"trace_on\": %d, \"traced\": %zu, \"calls_per_s\": %.1f, \"clock_window_us\": %.3f",
+           argv[1], k, m, cs, nd, reg ? 1 : 0, calls, traced ? 1 : 0, seg[8].size(), calls / dt, window * 1e-3);
+    for (int i = traced ? 0 : 8; i < 9; ++i)
         printf(", \"%s_us\": [%.3f, %.3f]", names[i], pct(seg[i], 0.5), pct(seg[i], 0.9));
     printf("}\n");
     if (reg) mec_host_unregister(slab);
