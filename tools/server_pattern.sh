@@ -16,7 +16,7 @@ mkdir -p "$OUT"
 g++ -std=c++11 -O2 -Wall -Imemec_amd/csrc/coding -Iinclude tools/coding_bench.cc memec_amd/csrc/coding/*.cc \
     -Lmemec_amd -lmec -Wl,-rpath,"$PWD/memec_amd" -lpthread -o tools/coding_bench || exit 1
 SECS=${SECS:-2}
-J=$OUT/server_pattern.jsonl
+J=${J:-$OUT/server_pattern.jsonl}
 : > "$J"
 for c in ${CFGS:-rs,4,2,4096 rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536}; do  # scheme,k,m,chunk
   cfg="$(echo $c | tr , ' ')"
