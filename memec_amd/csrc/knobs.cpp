@@ -10,13 +10,18 @@ namespace mec {
 namespace detail {
 namespace {
 
+// every knob's variable (the environment is read for each, once)
+constexpr const char *kEnvNames[] = {"MEC_SGROUP", "MEC_WINDOWS",      "MEC_BLOCK", "MEC_GBLOCK",  "MEC_GWPC",
+                                     "MEC_BM_VW",  "MEC_WPC",          "MEC_COPY_THREADS", "MEC_WIDE",
+                                     "MEC_MG_ROWS", "MEC_STAGGER"};
+// MEC_SGROUP sets two knobs (group and run), every other name one
+static_assert(sizeof(kEnvNames) / sizeof(kEnvNames[0]) == kKnobCount - 1, "a knob whose variable is never read");
+
 struct Knobs {
     std::atomic<int64_t> v[kKnobCount];
     Knobs() {
         for (auto &x : v) x.store(kKnobUnset, std::memory_order_relaxed);
-        for (const char *n : {"MEC_SGROUP", "MEC_WINDOWS", "MEC_BLOCK", "MEC_GBLOCK", "MEC_GWPC", "MEC_BM_VW",
-                              "MEC_WPC", "MEC_COPY_THREADS", "MEC_WIDE"})
-            apply(n, std::getenv(n));
+        for (const char *n : kEnvNames) apply(n, std::getenv(n));
     }
     bool apply(const char *name, const char *value) {
         auto put = [&](Knob k, int64_t x) { v[k].store(x, std::memory_order_relaxed); };

@@ -167,6 +167,21 @@ def test_knobs_through_the_api_not_the_environment():
     assert "getenv" not in src
 
 
+def test_every_knob_is_read_from_the_environment():
+    """knobs.cpp reads each knob's variable once at first use; a knob that
+    mec_set_knob accepts but the environment list misses is silently
+    ignored when set by variable (round 4: MEC_MG_ROWS / MEC_STAGGER were,
+    which voided an A/B run through the environment)."""
+    import re
+    src = open(os.path.join(ROOT, "memec_amd", "csrc", "knobs.cpp")).read()
+    env = set(re.findall(r'"(MEC_[A-Z_]+)"', src[src.index("kEnvNames[]"):src.index("};", src.index("kEnvNames[]"))]))
+    plain = set(re.findall(r'\{"(MEC_[A-Z_]+)", kKnob', src))
+    assert plain | {"MEC_SGROUP"} == env
+    hdr = open(os.path.join(ROOT, "include", "mec.h")).read()
+    for name in env:
+        assert name in hdr, name
+
+
 def test_probe_needs_a_context():
     L = _lib.lib()
     assert L.mec_set_probe(None, 1) == _lib.MEC_EINVAL
