@@ -34,7 +34,6 @@ struct Gf8Params {
     uint32_t sstride, dstride, chunk, s0;
     uint32_t units, tiles, accumulate, win;
     uint32_t nstr, sgroup, srun;  // stripes in this launch, stripe group and run (stripe_tile)
-    uint32_t stagger;             // != 0: s_sleep(32) between the arithmetic and the stores
     int64_t src_off[K];
     int64_t dst_off[R];
     Gf8Coef coef[R][K];
@@ -201,10 +200,6 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
 #pragma unroll
     for (int i = 0; i < R; ++i) acc[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off, true) : u32x4{0, 0, 0, 0};
     gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
-    // uniform; see gf8_stagger.  The branch is inside the asm: a C++ branch
-    // here splits the block and the compiler then keeps every bit field of
-    // the sources live across it (RS(10,4) dense 99 -> 272 VGPRs).
-    asm volatile("s_cmp_eq_u32 %0, 0\n\ts_cbranch_scc1 1f\n\ts_sleep 32\n1:" ::"s"(p.stagger) : "scc");
 #pragma unroll
     for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
 }
@@ -330,7 +325,6 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     p.nstr = 0;
     p.sgroup = 0;
     p.srun = 8;
-    p.stagger = 0;
     for (int j = 0; j < K; ++j) p.src_off[j] = L.src_off[j];
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int i = 0; i < R; ++i)
@@ -363,7 +357,6 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
                 const bool in_place = p.win > 1;
                 const dim3 grid(ns * g.tiles), block(bt);
                 const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, in_place, !vand, L.accumulate));
-                p.stagger = L.probe ? 0u : gf8_stagger(R, in_place, !vand, L.accumulate);
                 if (L.probe) {
                     if (bt == kWaveBlock)
                         hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Xor, kWaveBlock>), grid, block, lds, stream, p);

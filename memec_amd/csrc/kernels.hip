@@ -302,12 +302,6 @@ uint32_t ceil_even(double x) { return 2u * uint32_t(std::ceil(x / 2.0)); }
 uint32_t clampw(uint32_t w, uint32_t lo, uint32_t hi) { return std::min(hi, std::max(lo, w)); }
 }  // namespace
 
-uint32_t gf8_stagger(int rows, bool in_place, bool dense, bool accumulate) {
-    const int64_t e = knob(kKnobStagger);  // experiments (mec_set_knob)
-    if (e != kKnobUnset) return uint32_t(std::clamp<int64_t>(e, 0, 64));
-    return in_place && dense && !accumulate && rows == 4 ? 4u : 0u;
-}
-
 uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accumulate) {
     // read-modify-write of the outputs (delta updates, K = 1): each wave
     // also loads its R outputs; R = 2 / 3 / 4 want 16-18 / 12 / 10-12

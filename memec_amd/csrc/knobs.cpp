@@ -13,7 +13,7 @@ namespace {
 // every knob's variable (the environment is read for each, once)
 constexpr const char *kEnvNames[] = {"MEC_SGROUP", "MEC_WINDOWS",      "MEC_BLOCK", "MEC_GBLOCK",  "MEC_GWPC",
                                      "MEC_BM_VW",  "MEC_WPC",          "MEC_COPY_THREADS", "MEC_WIDE",
-                                     "MEC_MG_ROWS", "MEC_STAGGER"};
+                                     "MEC_MG_ROWS"};
 // MEC_SGROUP sets two knobs (group and run), every other name one
 static_assert(sizeof(kEnvNames) / sizeof(kEnvNames[0]) == kKnobCount - 1, "a knob whose variable is never read");
 
@@ -44,7 +44,7 @@ struct Knobs {
         } kPlain[] = {{"MEC_WINDOWS", kKnobWindows}, {"MEC_BLOCK", kKnobBlock},   {"MEC_GBLOCK", kKnobGblock},
                       {"MEC_GWPC", kKnobGwpc},       {"MEC_BM_VW", kKnobBmVw},     {"MEC_WPC", kKnobWpc},
                       {"MEC_COPY_THREADS", kKnobCopyThreads}, {"MEC_WIDE", kKnobWide},
-                      {"MEC_MG_ROWS", kKnobMgRows},  {"MEC_STAGGER", kKnobStagger}};
+                      {"MEC_MG_ROWS", kKnobMgRows}};
         for (const auto &p : kPlain)
             if (!std::strcmp(name, p.name)) {
                 put(p.k, num);

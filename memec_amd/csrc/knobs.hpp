@@ -24,7 +24,6 @@ enum Knob : int {
     kKnobCopyThreads, // MEC_COPY_THREADS=<n>
     kKnobWide,        // MEC_WIDE=0: > 4 outputs as 4-row launches (A/B of gf8_mg_kernel)
     kKnobMgRows,      // MEC_MG_ROWS=3|4|8: rows per group of gf8_mg_kernel
-    kKnobStagger,     // MEC_STAGGER=<n>: s_sleep(8) steps before a gf8 wave's stores
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

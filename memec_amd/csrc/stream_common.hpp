@@ -227,15 +227,6 @@ uint32_t gathered_lds(uint32_t bt, uint32_t static_lds, uint8_t gshape);
 // in active waves (waves that own units; a block of small packets can have
 // idle ones).  MEC_WPC=<n> overrides (0 = no cap): experiments flip it.
 uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accumulate);
-// s_sleep(8) steps a gf8 wave waits between its arithmetic and its stores.
-// The in-place dense decode (4 rows) stores right behind its loads at the
-// same stripe addresses; a ~2k-cycle pause spreads the waves' store bursts
-// and lifts RS(10,4)@1 MiB in-place decode 79.5 -> 80.3 % (the split
-// Vandermonde encode gets the same spacing from its longer arithmetic;
-// tools/stagger_probe.hip, profiles/r04/probes/stagger_probe_box2.log:
-// 16 steps of s_sleep(2..64) tried, 24-48 best).  0 elsewhere.  MEC_STAGGER=<n>
-// overrides (experiments).
-uint32_t gf8_stagger(int rows, bool in_place, bool dense, bool accumulate);
 // Bytes per lane per packet of a strided bitmatrix launch (16 or 8; w > 4
 // always 8).  A lane of the bitmatrix kernel reads the same slice of all w
 // packets of a chunk, so a wave touches w 1 KiB address slots (mod 8 KiB)

@@ -158,7 +158,7 @@ def test_knobs_through_the_api_not_the_environment():
     import memec_amd
     for name, value in (("MEC_WPC", "12"), ("MEC_SGROUP", "0"), ("MEC_SGROUP", "16:8"), ("MEC_BLOCK", "256"),
                         ("MEC_BM_VW", "2"), ("MEC_GBLOCK", "64"), ("MEC_GWPC", "0"), ("MEC_WINDOWS", "2"),
-                        ("MEC_COPY_THREADS", "4"), ("MEC_WIDE", "0"), ("MEC_MG_ROWS", "8"), ("MEC_STAGGER", "0")):
+                        ("MEC_COPY_THREADS", "4"), ("MEC_WIDE", "0"), ("MEC_MG_ROWS", "8")):
         memec_amd.set_knob(name, value)
         memec_amd.set_knob(name, None)
     with pytest.raises(MecError):
@@ -170,7 +170,7 @@ def test_knobs_through_the_api_not_the_environment():
 def test_every_knob_is_read_from_the_environment():
     """knobs.cpp reads each knob's variable once at first use; a knob that
     mec_set_knob accepts but the environment list misses is silently
-    ignored when set by variable (round 4: MEC_MG_ROWS / MEC_STAGGER were,
+    ignored when set by variable (round 4: MEC_MG_ROWS and a since-removed knob were,
     which voided an A/B run through the environment)."""
     import re
     src = open(os.path.join(ROOT, "memec_amd", "csrc", "knobs.cpp")).read()

@@ -94,27 +94,6 @@ def test_block_and_wave_cap_overrides(fam, block, wpc, knobs):
     _check_all_layouts(fam, 8192, 1300)
 
 
-@pytest.mark.parametrize("fam", ["rs", "isal_cauchy"])
-@pytest.mark.parametrize("stagger", ["0", "4", "16", None])
-def test_store_stagger(fam, stagger, knobs):
-    """The pause before a gf8 wave's stores (MEC_STAGGER; the rule's 4 steps
-    for 4-row in-place dense decodes) changes timing only: RS(10,4) decodes
-    of 4 erasures at 1 MiB-like strides and small chunks."""
-    knobs("MEC_STAGGER", stagger)
-    k, m = 10, 4
-    for cs, n in [(65536, 6), (4096, 9)]:
-        base = O.fill(n * (k + m) * cs, 3000 + cs % 991).reshape(n, k + m, cs)
-        for s in range(n):
-            base[s, k:] = np.stack(O.encode(fam, k, m, [base[s, j].copy() for j in range(k)], cs))
-        c = Codec(fam, k, m, cs)
-        st = torch.from_numpy(base.copy()).to("cuda")
-        st[:, :4] = 0
-        c.decode(st, sum(1 << i for i in range(4, k + m)))
-        torch.cuda.synchronize()
-        assert np.array_equal(st.cpu().numpy(), base), (fam, stagger, cs)
-        c.close()
-
-
 @pytest.mark.parametrize("stride_chunk", [2048, 65536])
 def test_power_of_two_stripe_strides(stride_chunk):
     """RS(6,2) stripes are 8 chunks: 16 KiB and 512 KiB strides, the two

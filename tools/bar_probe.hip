@@ -104,6 +104,29 @@ __global__ void desc_kernel(const u32x4 *in, uint64_t *ticks, uint32_t *sink, in
     sink[threadIdx.x] = acc;
 }
 
+// release cost: 256 lanes store `bytes` to pinned host memory (one job's
+// output), wait for the acks, barrier, then thread 0 times a system-scope
+// release fence (the L2 writeback the queue's done store pays) and the
+// done store after it; n rounds, ticks of the fence and of the fence+store
+__global__ void release_kernel(uint32_t *out, uint32_t words, uint32_t *done, uint64_t *ticks, int n) {
+    for (int i = 0; i < n; ++i) {
+        for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) out[w] = uint32_t(i) ^ w;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            __hip_atomic_store(done, uint32_t(i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+            ticks[2 * i] = t1 - t0;
+            ticks[2 * i + 1] = t2 - t0;
+        }
+        __syncthreads();
+    }
+}
+
 struct Place {
     const char *name;
     uint32_t *host;  // CPU address
@@ -201,6 +224,30 @@ int main(int argc, char **argv) {
                "\"device_misses\": %u, \"host_misses\": %d}\n",
                desc_us, rt[rt.size() / 2], rt[rt.size() / 10], rt[rt.size() * 9 / 10], dmiss, host_miss);
         fflush(stdout);
+    }
+    // release cost after a 4 KiB job output to pinned host memory
+    {
+        uint32_t *oh = nullptr, *od = nullptr;
+        CK(hipHostMalloc((void **)&oh, 1 << 16, hipHostMallocMapped | hipHostMallocCoherent));
+        CK(hipHostGetDevicePointer((void **)&od, oh, 0));
+        uint64_t *rt = nullptr;
+        CK(hipMalloc((void **)&rt, 2 * 256 * sizeof(uint64_t)));
+        for (uint32_t bytes : {4096u, 65536u}) {
+            hipLaunchKernelGGL(release_kernel, dim3(1), dim3(256), 0, st, od, bytes / 4, out_d, rt, 256);
+            CK(hipStreamSynchronize(st));
+            std::vector<uint64_t> t(512);
+            CK(hipMemcpy(t.data(), rt, t.size() * 8, hipMemcpyDeviceToHost));
+            std::vector<double> f, fs;
+            for (int i = 1; i < 256; ++i) {
+                f.push_back(t[2 * i] * ns_per_tick * 1e-3);
+                fs.push_back(t[2 * i + 1] * ns_per_tick * 1e-3);
+            }
+            std::sort(f.begin(), f.end());
+            std::sort(fs.begin(), fs.end());
+            printf("{\"release_after_output_bytes\": %u, \"release_fence_us_median\": %.3f, \"fence_plus_done_store_acked_us_median\": %.3f}\n",
+                   bytes, f[f.size() / 2], fs[fs.size() / 2]);
+            fflush(stdout);
+        }
     }
     return 0;
 }
