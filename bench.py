@@ -651,6 +651,81 @@ def load_traffic(cfg_name, stripes):
                                           "gfx950-corrected; not measured in this run)" % (cfg_name, tag))
 
 
+def under_profiler():
+    """True inside a rocprofv3 run (its tool library is preloaded), where
+    the live PMC passes below would nest one profiler in another."""
+    return "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
+
+
+def pmc_per_launch(path, counter):
+    """Counter average per launch of the dominant coding kernel in a
+    rocprofv3 --pmc CSV (the kernel launched most often; fills and the XOR
+    twin excluded), as tools/pmc_summary.py."""
+    import csv
+    by_name = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            name = row["Kernel_Name"]
+            if row["Counter_Name"] != counter or re.search(r"gf8_kernel<\d+, \d+, (true|false), 2,", name):
+                continue
+            if "gf8_kernel" in name or "gf8_mg_kernel" in name or "bm_kernel" in name:
+                by_name.setdefault(name, []).append(float(row["Counter_Value"]))
+    if not by_name:
+        return None, None
+    name = max(by_name, key=lambda n: len(by_name[n]))
+    return sum(by_name[name]) / len(by_name[name]), name
+
+
+def live_traffic(cfg_name, stripes, timeout=240):
+    """HBM bytes per launch of this config's coding kernel, measured in this
+    run: two child processes of this script, each under `rocprofv3 --pmc`
+    with one counter (FETCH_SIZE, then WRITE_SIZE; separate passes, as
+    MI355X_MICROARCH.md prescribes), started before this process touches
+    the GPU.  gfx950 correction: read bytes = 2 x FETCH_SIZE KiB (a wide
+    streaming read is counted at half), write bytes = WRITE_SIZE KiB.
+    Returns (bytes, detail) or (None, reason); never raises."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3") or ("/opt/rocm/bin/rocprofv3" if os.path.exists("/opt/rocm/bin/rocprofv3") else None)
+    if not exe:
+        return None, "rocprofv3 not found"
+    kib = {}
+    kernel = None
+    with tempfile.TemporaryDirectory(prefix="mec_pmc_") as tmp:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
+                   os.path.abspath(__file__), "--config", cfg_name, "--stripes", str(stripes), "--steps", "3",
+                   "--warmup", "1", "--no-cpu-baseline", "--no-extra-configs", "--no-ceiling", "--no-secondary",
+                   "--no-pmc-live"]
+            try:
+                with open(os.path.join(tmp, counter + ".log"), "w") as log:
+                    p = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+                    try:
+                        rc = p.wait(timeout=timeout)
+                    except subprocess.TimeoutExpired:
+                        os.killpg(p.pid, signal.SIGKILL)
+                        p.wait()
+                        return None, "rocprofv3 %s pass timed out after %d s" % (counter, timeout)
+            except OSError as exc:
+                return None, "rocprofv3 %s pass did not start: %r" % (counter, exc)
+            if rc != 0:
+                return None, "rocprofv3 %s pass exited %d" % (counter, rc)
+            path = os.path.join(d, "run_counter_collection.csv")
+            if not os.path.exists(path):
+                return None, "rocprofv3 %s pass wrote no counter CSV" % counter
+            kib[counter], kernel = pmc_per_launch(path, counter)
+            if kib[counter] is None:
+                return None, "no coding kernel in the %s pass" % counter
+    rd, wr = 2 * kib["FETCH_SIZE"] * 1024, kib["WRITE_SIZE"] * 1024
+    return rd + wr, {"read_bytes": rd, "write_bytes": wr, "kernel": kernel,
+                     "source": "live: two child runs of this config (%d stripes, 3 steps) under rocprofv3 --pmc "
+                               "FETCH_SIZE / --pmc WRITE_SIZE, started before this process touched the GPU; read = "
+                               "2 x FETCH_SIZE KiB (gfx950 wide-stream halving), write = WRITE_SIZE KiB" % stripes}
+
+
 def launcher_cmd(argv, gpus, port, python=None):
     """The command that starts `gpus` rank processes of this script (one per
     GPU) when bench.py is run as `python bench.py --gpus N` without a
@@ -840,6 +915,9 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="also time the host-memory (PCIe) batch encode")
     ap.add_argument("--strong", action="store_true",
                     help="--stripes is the global batch, sharded over ranks (default: per-GPU batch, weak scaling)")
+    ap.add_argument("--no-pmc-live", action="store_true",
+                    help="read roofline.traffic from profiles/pmc_<config>.json instead of measuring it "
+                         "(rocprofv3 --pmc child passes before the run; N = 1 only)")
     ap.add_argument("--dist-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -871,6 +949,16 @@ def main():
         return
 
     from memec_amd import Codec, fill_random
+
+    # roofline.traffic measured live: PMC passes in child processes, before
+    # this process touches the GPU (N = 1, plain runs, not under a profiler)
+    pmc_live = None
+    if (world == 1 and "WORLD_SIZE" not in os.environ and not args.no_pmc_live and not under_profiler()
+            and os.environ.get("MEC_BENCH_PMC_LIVE", "1") != "0"):
+        pmc_live = live_traffic(args.config, args.stripes or CONFIGS[args.config][4])
+        if pmc_live[0] is None:
+            print("bench: live PMC traffic unavailable (%s); using the committed profile" % pmc_live[1],
+                  file=sys.stderr, flush=True)
 
     # MEC_BENCH_DIST_BACKEND=gloo rehearses the multi-rank harness on fewer
     # GPUs than ranks (ranks share devices round-robin); the real run is
@@ -1116,6 +1204,13 @@ def main():
         dist.barrier()
     if rank == 0:
         traffic, traffic_src = load_traffic(args.config, stripes)
+        traffic_committed = traffic
+        traffic_detail = None
+        if pmc_live and pmc_live[0] is not None:
+            traffic, traffic_detail = pmc_live
+            traffic_src = traffic_detail["source"]
+        elif pmc_live:
+            traffic_src = "%s; live PMC passes unavailable: %s" % (traffic_src, pmc_live[1])
         # data GiB/s: k data chunks per stripe (encode / decode), the one
         # delta chunk per stripe for updates
         value = global_stripes * (cs if op == "update" else k * cs) * args.steps / wall / 2**30
@@ -1139,6 +1234,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
+                         "traffic_over_algorithmic": round(traffic / alg_bytes, 4) if traffic else None,
+                         "traffic_read_write": [traffic_detail["read_bytes"], traffic_detail["write_bytes"]]
+                         if traffic_detail else None,
+                         "traffic_committed_profile": traffic_committed if traffic_detail else None,
                          "algorithmic_bytes_per_launch": alg_bytes, "kernel_ms": round(kern_ms, 4),
                          "xor_twin_GBps": round(twin_gbps, 1) if twin_gbps else None,
                          "frac_of_xor_twin": round(achieved / twin_gbps, 4) if twin_gbps else None,

@@ -78,3 +78,34 @@ def test_default_line_pins_parity_on_every_timed_config():
         assert c["parity"]["equal"], name
         if "decode" in c:
             assert c["decode"]["parity"]["equal"], name
+
+
+def test_bench_live_pmc_parser_matches_the_committed_summary():
+    """bench.py measures roofline.traffic live (rocprofv3 --pmc child passes,
+    bench.live_traffic); its CSV parser must give the same per-launch
+    counters as tools/pmc_summary.py gave for the committed profile."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    fetch = os.path.join(ROOT, "profiles", "r04", "final", "pmc", "pmc_fetch_rs_enc.csv")
+    write = os.path.join(ROOT, "profiles", "r04", "final", "pmc", "pmc_write_rs_enc.csv")
+    if not (os.path.exists(fetch) and os.path.exists(write)):
+        pytest.skip("round-4 PMC CSVs not present")
+    j = json.load(open(os.path.join(ROOT, "profiles", "pmc_rs_enc.json")))
+    f, name = bench.pmc_per_launch(fetch, "FETCH_SIZE")
+    w, _ = bench.pmc_per_launch(write, "WRITE_SIZE")
+    assert "gf8_kernel<10, 4, false, 1, 64>" in name
+    assert f == pytest.approx(j["FETCH_SIZE_kib_per_launch"], rel=1e-12)
+    assert w == pytest.approx(j["WRITE_SIZE_kib_per_launch"], rel=1e-12)
+
+
+def test_bench_skips_live_pmc_under_a_profiler(monkeypatch):
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.delenv("LD_PRELOAD", raising=False)
+    for k in [k for k in os.environ if k.startswith("ROCPROF")]:
+        monkeypatch.delenv(k)
+    assert not bench.under_profiler()
+    monkeypatch.setenv("LD_PRELOAD", "/opt/rocm/lib/rocprofiler-sdk/librocprofiler-sdk-tool.so")
+    assert bench.under_profiler()
