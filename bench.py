@@ -657,6 +657,15 @@ def under_profiler():
     return "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
 
 
+def wants_live_pmc(world, disabled):
+    """Live PMC passes only for the plain single-process run (no launcher,
+    no profiler around it, not turned off by --no-pmc-live or
+    MEC_BENCH_PMC_LIVE=0): the child passes must start before this process
+    touches the GPU, and a multi-rank job leaves the counters to N = 1."""
+    return (world < 2 and "WORLD_SIZE" not in os.environ and not disabled and not under_profiler()
+            and os.environ.get("MEC_BENCH_PMC_LIVE", "1") != "0")
+
+
 def pmc_per_launch(path, counter):
     """Counter average per launch of the dominant coding kernel in a
     rocprofv3 --pmc CSV (the kernel launched most often; fills and the XOR
@@ -953,8 +962,7 @@ def main():
     # roofline.traffic measured live: PMC passes in child processes, before
     # this process touches the GPU (N = 1, plain runs, not under a profiler)
     pmc_live = None
-    if (world == 1 and "WORLD_SIZE" not in os.environ and not args.no_pmc_live and not under_profiler()
-            and os.environ.get("MEC_BENCH_PMC_LIVE", "1") != "0"):
+    if wants_live_pmc(world, args.no_pmc_live):
         pmc_live = live_traffic(args.config, args.stripes or CONFIGS[args.config][4])
         if pmc_live[0] is None:
             print("bench: live PMC traffic unavailable (%s); using the committed profile" % pmc_live[1],
