@@ -1,6 +1,6 @@
 """The committed measurement evidence agrees with itself (CPU, no GPU).
 
-bench.py's `roofline.traffic` is read from profiles/pmc_<config>.json, and
+bench.py's `roofline.traffic` falls back to profiles/pmc_<config>.json (live PMC passes otherwise), and
 DESIGN quotes the default command's line next to the rocprofv3 kernel
 averages of the same run (profiles/rNN/final/, the newest round).  These checks keep those
 files consistent: PMC traffic equals the algorithmic bytes, and every timed
