@@ -55,14 +55,15 @@ def test_geometry_sweep_vs_oracle(fam):
     _sweep(fam, _shapes(fam, 40, 0xC0DE + FAMS.index(fam)), random.Random(0x5EED + FAMS.index(fam)), 2)
 
 
-@pytest.mark.skipif(not os.environ.get("MEC_SWEEP_EXTENDED"), reason="one-off extended sweep (MEC_SWEEP_EXTENDED=<shapes>)")
 @pytest.mark.parametrize("fam", FAMS)
 def test_geometry_sweep_extended(fam):
-    """The same check over MEC_SWEEP_EXTENDED shapes per family with chunks
-    of 8 B-64 KiB (every launch shape the rules pick: one-wave / 4-wave
-    blocks, 8- / 16-byte bitmatrix lanes, the tiny in-place rule, tails),
-    another seed; run on demand, its log kept under profiles/."""
-    count = int(os.environ["MEC_SWEEP_EXTENDED"])
+    """The same check over 1000 shapes per family (MEC_SWEEP_EXTENDED=<n>
+    for more; 3000 in profiles/r04/parity/sweep_extended_3000.log) with
+    chunks of 8 B-64 KiB: every launch shape the rules pick (one-wave /
+    4-wave blocks, 8- / 16-byte bitmatrix lanes, the tiny in-place rule,
+    tails, one-pass wide codes with groups of 3, 4 and 8 rows), another
+    seed.  ~15 s per family on the MI355X."""
+    count = int(os.environ.get("MEC_SWEEP_EXTENDED") or 1000)
     _sweep(fam, _shapes(fam, count, 0xE77 + FAMS.index(fam), max_units=8192), random.Random(0xE5 + FAMS.index(fam)), 3)
 
 
