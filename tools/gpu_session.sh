@@ -89,16 +89,6 @@ for step in "$@"; do
             run stagger_pmc_c 200 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU \
                 SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/stagger_pmc_c" -o run -- tools/stagger_probe 2048 1 "$arms"
             python3 tools/stagger_pmc.py "$arms" "$OUT/stagger_pmc_a" "$OUT/stagger_pmc_b" "$OUT/stagger_pmc_c" > "$OUT/stagger_pmc.jsonl" ;;
-        staggerab)  # the store stagger rule against MEC_STAGGER=0, decode configs, interleaved
-            for r in 1 2; do
-                for c in ${STAGGER_CONFIGS:-rs_dec rs_dec_mixed}; do
-                    for st in rule 0 6; do
-                        if [ $st = rule ]; then e=MEC_STAGGER_UNSET=1; else e=MEC_STAGGER=$st; fi
-                        run "stagger_${c}_${st}_$r" 200 env $e python bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 10
-                        grep -h '^{' "$OUT/stagger_${c}_${st}_$r.log" | sed "s/^{/{\"stagger\": \"$st\", \"round\": $r, /" >> "$OUT/staggerab.jsonl"
-                    done
-                done
-            done ;;
         mixed)
             for w in 1 4 16; do
                 run "mixed_w$w" 120 tools/mixed_ab 1024 $w 3 32
