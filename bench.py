@@ -685,7 +685,7 @@ def pmc_per_launch(path, counter):
     return sum(by_name[name]) / len(by_name[name]), name
 
 
-def live_traffic(cfg_name, stripes, timeout=240):
+def live_traffic(cfg_name, stripes, timeout=120):
     """HBM bytes per launch of this config's coding kernel, measured in this
     run: two child processes of this script, each under `rocprofv3 --pmc`
     with one counter (FETCH_SIZE, then WRITE_SIZE; separate passes, as
