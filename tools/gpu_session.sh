@@ -79,6 +79,21 @@ for step in "$@"; do
         stagger) run stagger_probe 300 tools/stagger_probe 4096 3 ;;
         wider8) run wide_r8_probe 300 tools/wide_r8_probe 16384 3 ;;
         bar) run bar_probe 120 tools/bar_probe 2000 ;;
+        asan)  # host-ASan build (tools/asan_build.sh, built beforehand): the server pattern and queue calls
+            export ASAN_OPTIONS=detect_leaks=0:abort_on_error=1
+            for c in rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536 rs,6,3,20504; do
+                for mode in seal delta decode; do
+                    for w in 1 16; do
+                        for reg in 0 1; do
+                            run "asan_$(echo $c | tr , _)_${mode}_w${w}_r$reg" 90 env MEMEC_GPU_REGISTER=$reg \
+                                tools/coding_bench_asan $(echo $c | tr , ' ') $w 1 $mode
+                        done
+                    done
+                done
+            done
+            run asan_latency_rs 120 tools/queue_latency_asan rs 8 2 4096 3000 1 1
+            run asan_latency_cauchy 120 tools/queue_latency_asan cauchy 4 2 4096 3000 0 2
+            grep -l "ERROR: AddressSanitizer" "$OUT"/asan_*.log > "$OUT/asan_errors.txt" || true ;;
         staggerpmc)  # EA counters per stagger_probe arm (tools/stagger_pmc.py)
             arms=${STAGGER_ARMS:-split_enc,split_twin_cap12,split_dense_cap12,inplace_dec,inplace_dec_sleep32,inplace_twin,inplace_vand}
             run stagger_plain 200 tools/stagger_probe 2048 1 "$arms"
