@@ -79,6 +79,17 @@ for step in "$@"; do
         stagger) run stagger_probe 300 tools/stagger_probe 4096 3 ;;
         wider8) run wide_r8_probe 300 tools/wide_r8_probe 16384 3 ;;
         bar) run bar_probe 120 tools/bar_probe 2000 ;;
+        tsan)  # host-TSan build (tools/tsan_build.sh, built beforehand): concurrent callers
+            export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0"
+            for c in rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536; do
+                for mode in seal decode; do
+                    for reg in 0 1; do
+                        run "tsan_$(echo $c | tr , _)_${mode}_r$reg" 120 env MEMEC_GPU_REGISTER=$reg \
+                            tools/coding_bench_tsan $(echo $c | tr , ' ') 16 1 $mode
+                    done
+                done
+            done
+            grep -c "WARNING: ThreadSanitizer" "$OUT"/tsan_*.log > "$OUT/tsan_counts.txt" || true ;;
         asan)  # host-ASan build (tools/asan_build.sh, built beforehand): the server pattern and queue calls
             export ASAN_OPTIONS=detect_leaks=0:abort_on_error=1
             for c in rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536 rs,6,3,20504; do

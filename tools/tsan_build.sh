@@ -1,0 +1,38 @@
+#!/usr/bin/env bash
+# tools/tsan_build.sh — a host-ThreadSanitizer build of libmec and of two
+# host-side drivers, for runs on the GPU box (device code unchanged: every
+# -fsanitize flag applies to the host side only, -Xarch_host).
+#   memec_amd/tsan/libmec.so      every csrc unit, host code instrumented
+#   tools/coding_bench_tsan       MemEC's calling pattern through the adapter
+#   tools/queue_latency_tsan      single-caller queue calls, traced
+# The ASan runtime is linked statically into the two executables (clang's
+# default), so no preload is involved.  Run with
+#   TSAN_OPTIONS=halt_on_error=0 (reports to stderr)
+set -eu
+cd "$(dirname "$0")/.."
+HIPCC=/opt/rocm/bin/hipcc
+CLANG=/opt/rocm/llvm/bin/clang++
+ASAN="-Xarch_host -fsanitize=thread -Xarch_host -fno-omit-frame-pointer"
+OUT=memec_amd/build_tsan
+LIB=memec_amd/tsan
+mkdir -p "$OUT" "$LIB"
+FLAGS="--offload-arch=gfx950 --offload-compress -O2 -g -std=c++17 -fPIC -Wall -Iinclude -Imemec_amd/csrc $ASAN"
+objs=()
+pids=()
+for f in memec_amd/csrc/*.hip memec_amd/csrc/*.cpp; do
+    o="$OUT/$(basename "${f%.*}").o"
+    objs+=("$o")
+    if [ ! -f "$o" ] || [ "$f" -nt "$o" ]; then
+        $HIPCC $FLAGS -c -o "$o" "$f" &
+        pids+=($!)
+        if [ ${#pids[@]} -ge 8 ]; then wait "${pids[0]}"; pids=("${pids[@]:1}"); fi
+    fi
+done
+for p in "${pids[@]}"; do wait "$p"; done
+$HIPCC --offload-arch=gfx950 -shared -fPIC -o "$LIB/libmec.so" "${objs[@]}" -Wl,-soname,libmec.so
+$CLANG -std=c++11 -O1 -g -fsanitize=thread -fno-omit-frame-pointer -Imemec_amd/csrc/coding -Iinclude \
+    tools/coding_bench.cc memec_amd/csrc/coding/*.cc -L"$LIB" -lmec -Wl,-rpath,'$ORIGIN/../memec_amd/tsan' \
+    -lpthread -o tools/coding_bench_tsan
+$HIPCC --offload-arch=gfx950 -O1 -g -std=c++17 -Iinclude $ASAN tools/queue_latency.hip -L"$LIB" -lmec \
+    -Wl,-rpath,'$ORIGIN/../memec_amd/tsan' -o tools/queue_latency_tsan
+echo "tsan build done"
