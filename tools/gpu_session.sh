@@ -80,7 +80,7 @@ for step in "$@"; do
         wider8) run wide_r8_probe 300 tools/wide_r8_probe 16384 3 ;;
         bar) run bar_probe 120 tools/bar_probe 2000 ;;
         tsan)  # host-TSan build (tools/tsan_build.sh, built beforehand): concurrent callers
-            export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0"
+            export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 exitcode=0 suppressions=$PWD/tools/tsan_suppressions.txt"
             for c in rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536; do
                 for mode in seal decode; do
                     for reg in 0 1; do
