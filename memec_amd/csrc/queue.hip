@@ -522,12 +522,21 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     q->solo_max = uint32_t(env_u64("MEC_QUEUE_SOLO_MAX", q->max_chunk));
     q->idle_ticks = env_u64("MEC_QUEUE_IDLE_MS", 50) * 100000ull;  // s_memrealtime: 100 MHz
     q->timeout_ms = env_u64("MEC_QUEUE_TIMEOUT_MS", 5000);
-    // workgroups per slot: one per MEC_QUEUE_PART_THREADS units (default
-    // kQThreads: a 16 KiB pass of 16-byte units), at most kQMaxParts;
-    // MEC_QUEUE_PARTS sets the count directly (A/Bs)
+    // workgroups per slot: one per 16 KiB of chunk (a kQThreads pass of
+    // 16-byte units), and below 64 KiB one per 8 KiB up to 4 — a lone
+    // caller's sources then stream over PCIe through more CUs: one caller's
+    // RS(8,2)@16 KiB calls 68 -> 82 K/s with 2 parts (96 K with 4, but 16
+    // callers lose 5 % there), while 64 KiB is fastest at 4 parts for one
+    // and for 16 callers (profiles/r04/host/queue_parts_ab.jsonl); at most
+    // kQMaxParts.  MEC_QUEUE_PART_THREADS=<n> sets one part per n units,
+    // MEC_QUEUE_PARTS the count directly (A/Bs)
     const uint32_t units = (c->cs + 15) / 16;
-    const uint32_t pthr = uint32_t(std::min<uint64_t>(kQThreads, std::max<uint64_t>(64, env_u64("MEC_QUEUE_PART_THREADS", kQThreads))));
-    const uint32_t auto_parts = std::min<uint32_t>(kQMaxParts, std::max<uint32_t>(1, (units + pthr - 1) / pthr));
+    uint32_t auto_parts = std::max((units + kQThreads - 1) / kQThreads, std::min(4u, (units + 511) / 512));
+    if (std::getenv("MEC_QUEUE_PART_THREADS")) {
+        const uint32_t pthr = uint32_t(std::min<uint64_t>(kQThreads, std::max<uint64_t>(64, env_u64("MEC_QUEUE_PART_THREADS", kQThreads))));
+        auto_parts = (units + pthr - 1) / pthr;
+    }
+    auto_parts = std::min<uint32_t>(kQMaxParts, std::max<uint32_t>(1, auto_parts));
     q->parts = std::min<uint32_t>(kQMaxParts, std::max<uint64_t>(1, env_u64("MEC_QUEUE_PARTS", auto_parts)));
     // one 16-byte unit per thread up to kQThreads (a 4 KiB chunk: 256 threads;
     // idle threads only cost barrier time), at least 128 (descriptor loads)

@@ -108,7 +108,15 @@ def test_queue_cauchy_packet_tails(k, m, cs):
     _encode_decode_update("cauchy", k, m, cs)
 
 
-def _encode_decode_update(fam, k, m, cs, parts=1, slots=8):
+def auto_parts(cs):
+    """queue_start's rule: one part per 16 KiB of chunk, below 64 KiB one
+    per 8 KiB up to 4 (queue.hip)."""
+    units = (cs + 15) // 16
+    return min(64, max(1, (units + 1023) // 1024, min(4, (units + 511) // 512)))
+
+
+def _encode_decode_update(fam, k, m, cs, parts=None, slots=8):
+    parts = auto_parts(cs) if parts is None else parts
     slab = Slab(k + m + 1, cs, 31 + k)
     c = Codec(fam, k, m, cs)
     try:
@@ -177,7 +185,7 @@ def test_queue_multi_part_slots(fam, k, m, cs, qenv):
     the slot's parts (workgroups on different CUs), each with its own done
     word; partial units and bitmatrix packet tails land on the right part."""
     qenv(MEC_QUEUE_MAX_CHUNK=128 << 10)
-    _encode_decode_update(fam, k, m, cs, parts=(cs // 16 + 1023) // 1024)
+    _encode_decode_update(fam, k, m, cs)
 
 
 @pytest.mark.parametrize("fam", ["rs", "cauchy"])
