@@ -527,7 +527,8 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     // caller's sources then stream over PCIe through more CUs: one caller's
     // RS(8,2)@16 KiB calls 68 -> 82 K/s with 2 parts (96 K with 4, but 16
     // callers lose 5 % there), while 64 KiB is fastest at 4 parts for one
-    // and for 16 callers (profiles/r04/host/queue_parts_ab.jsonl); at most
+    // and for 16 callers (profiles/r04/host/queue_parts_ab.jsonl,
+    // queue_parts_rule_ab.jsonl: 16 KiB 68 -> 84 K/s, 16 callers equal); at most
     // kQMaxParts.  MEC_QUEUE_PART_THREADS=<n> sets one part per n units,
     // MEC_QUEUE_PARTS the count directly (A/Bs)
     const uint32_t units = (c->cs + 15) / 16;
