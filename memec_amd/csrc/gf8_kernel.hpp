@@ -406,9 +406,13 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
         p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
         p.nstr = ns;
         p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
-        // the tables are the block's LDS; the wave cap may reserve more
-        const uint32_t cap = occupancy_lds(kWaveBlock, kWaveBlock, 0,
-                                           gf8_target_waves(K, L.rows, p.win > 1, !L.vand, L.accumulate));
+        // the tables are the block's LDS, and no wave cap: the caps of the
+        // <= 4-row launches (gf8_target_waves) starve these longer-computing
+        // waves — uncapped, RS(10,6)@256 KiB 67.2 -> 72.3 %, RS(8,5)@16 KiB
+        // 63.6 -> 66.5, ISA-L RS(12,8) 65.8 -> 67.2, the rest within 0.3
+        // (tools/wide_ab.py, profiles/r04/wide/mg_wpc_ab*.jsonl); MEC_WPC
+        // still forces one (experiments)
+        const uint32_t cap = occupancy_lds(kWaveBlock, kWaveBlock, 0, 0);
         const uint32_t lds = std::max(cap, tab_bytes);
         if (L.vand)
             hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Vand>), dim3(ns * g.tiles), dim3(kWaveBlock), lds, stream, p);

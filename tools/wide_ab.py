@@ -21,7 +21,9 @@ sys.path.insert(0, ROOT)
 
 SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384, "encode"),
           ("rs", 16, 8, 65536, 16384, "decode"), ("rs", 10, 6, 262144, 4096, "encode"),
-          ("isal_cauchy", 12, 6, 65536, 16384, "encode")]
+          ("isal_cauchy", 12, 6, 65536, 16384, "encode"), ("rs", 8, 5, 16384, 32768, "encode"),
+          ("isal_cauchy", 20, 8, 4096, 65536, "encode"), ("rs", 10, 6, 262144, 4096, "decode"),
+          ("rs", 4, 12, 1 << 20, 512, "encode")]
 
 
 def run(mode, steps, warmup, shapes):
