@@ -350,6 +350,11 @@ uint32_t bm_lane_bytes(int w, int rows, uint64_t chunk, bool in_place) {
 }
 
 uint32_t bm_target_waves(int rows, int w, int vw, bool in_place) {
+    // more than 4 outputs (wide codes): no cap — such a wave keeps rows x w
+    // packet slices and computes long enough that the caps below starve the
+    // stream (Cauchy(10,6)@64 KiB encode 74.6 -> 79.3 %, its in-place
+    // decode unchanged; tools/wide_ab.py, profiles/r04/wide/bm_wpc_ab.jsonl)
+    if (rows > 4) return 0;
     // w > 4 always runs 8-byte slices of twice as many packets: the
     // 16-byte rule's bytes in flight per wave
     if (vw >= 4 || w > 4) return clampw(uint32_t(3 * rows), 6, 16);

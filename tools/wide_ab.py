@@ -23,7 +23,9 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("rs", 16, 8, 65536, 16384, "decode"), ("rs", 10, 6, 262144, 4096, "encode"),
           ("isal_cauchy", 12, 6, 65536, 16384, "encode"), ("rs", 8, 5, 16384, 32768, "encode"),
           ("isal_cauchy", 20, 8, 4096, 65536, "encode"), ("rs", 10, 6, 262144, 4096, "decode"),
-          ("rs", 4, 12, 1 << 20, 512, "encode")]
+          ("rs", 4, 12, 1 << 20, 512, "encode"), ("cauchy", 10, 6, 65536, 16384, "encode"),
+          ("cauchy", 10, 6, 65536, 16384, "decode"), ("cauchy", 8, 5, 16384, 32768, "encode"),
+          ("cauchy", 20, 8, 40960, 8192, "encode"), ("cauchy", 20, 8, 40960, 8192, "decode")]
 
 
 def run(mode, steps, warmup, shapes):
