@@ -353,7 +353,8 @@ uint32_t bm_target_waves(int rows, int w, int vw, bool in_place) {
     // more than 4 outputs (wide codes): no cap — such a wave keeps rows x w
     // packet slices and computes long enough that the caps below starve the
     // stream (Cauchy(10,6)@64 KiB encode 74.6 -> 79.3 %, its in-place
-    // decode unchanged; tools/wide_ab.py, profiles/r04/wide/bm_wpc_ab.jsonl)
+    // decode unchanged, Cauchy(8,5)@16 KiB +2.8, Cauchy(20,8) equal;
+    // tools/wide_ab.py, profiles/r04/wide/bm_wpc_ab*.jsonl)
     if (rows > 4) return 0;
     // w > 4 always runs 8-byte slices of twice as many packets: the
     // 16-byte rule's bytes in flight per wave
