@@ -25,7 +25,10 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("isal_cauchy", 20, 8, 4096, 65536, "encode"), ("rs", 10, 6, 262144, 4096, "decode"),
           ("rs", 4, 12, 1 << 20, 512, "encode"), ("cauchy", 10, 6, 65536, 16384, "encode"),
           ("cauchy", 10, 6, 65536, 16384, "decode"), ("cauchy", 8, 5, 16384, 32768, "encode"),
-          ("cauchy", 20, 8, 40960, 8192, "encode"), ("cauchy", 20, 8, 40960, 8192, "decode")]
+          ("cauchy", 20, 8, 40960, 8192, "encode"), ("cauchy", 20, 8, 40960, 8192, "decode"),
+          ("rs", 16, 8, 65536, 16384, "batch"), ("isal_rs", 12, 8, 65536, 16384, "batch"),
+          ("cauchy", 10, 6, 65536, 16384, "batch"), ("rs", 10, 4, 1 << 20, 4096, "batch"),
+          ("rs", 10, 4, 1 << 20, 4096, "encode")]
 
 
 def run(mode, steps, warmup, shapes):
@@ -38,9 +41,15 @@ def run(mode, steps, warmup, shapes):
         c = Codec(fam, k, m, cs)
         data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
         fill_random(data, 1234)
-        if op == "encode":
+        if op in ("encode", "batch"):
             par = torch.empty(n, m, cs, dtype=torch.uint8, device="cuda")
-            step = lambda: c.encode(data, par)  # noqa: E731
+            if op == "encode":
+                step = lambda: c.encode(data, par)  # noqa: E731
+            else:  # the pointer-array ABI (mec_encode_batch) over the same chunks
+                db, pb = data.data_ptr(), par.data_ptr()
+                dptr = [db + (s * k + j) * cs for s in range(n) for j in range(k)]
+                pptr = [pb + (s * m + i) * cs for s in range(n) for i in range(m)]
+                step = lambda: c.encode_batch(dptr, pptr, mem="device")  # noqa: E731
             alg = (k + m) * cs * n
             result = lambda: par  # noqa: E731
         else:
