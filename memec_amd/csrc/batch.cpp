@@ -302,9 +302,14 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
     // anything else through per-stripe descriptors (and byte-wise maps with
     // more than 4 outputs too: the descriptor kernel codes every row group
     // from one read of the sources)
-    bool single = M.ssel.size() == 1 && M.rows() <= size_t(kMaxRows);
-    if (single && pat)
-        for (uint32_t s = 0; s < n && single; ++s) single = pat[s] == 0;
+    bool one_map = M.ssel.size() == 1;
+    if (one_map && pat)
+        for (uint32_t s = 0; s < n && one_map; ++s) one_map = pat[s] == 0;
+    // one map and more than 4 byte-wise outputs: the one-pass kernel reads
+    // the pointer rows itself, with the map's tables and structure (row 0 /
+    // column 0 XORs, groups of 3, 4 or 8) like a strided launch
+    const bool one_pass = one_map && M.K >= 1 && mg_wanted(c, M.rows());
+    const bool single = one_map && (M.rows() <= size_t(kMaxRows) || one_pass);
     std::vector<uint32_t> descs;
     uint32_t desc_dw = 0;
     const size_t groups = single ? 0 : build_descs(c, M, descs, desc_dw);
@@ -328,6 +333,24 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
         // (gf8_kernel / bm_kernel gather mode), only the pointers are read
         const std::vector<uint8_t> &ss = M.ssel[0], &ds = M.dsel[0];
         const Mat &cf = M.coef[0];
+        if (one_pass) {
+            Gf8MgLaunch L{};
+            L.stab = dstab;
+            L.dtab = ddtab;
+            L.sstride = sstride;
+            L.dstride = dstride;
+            L.k = int(M.K);
+            L.rows = int(ds.size());
+            L.len = c->cs;
+            L.n_stripes = n;
+            L.accumulate = M.accumulate;
+            for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
+            for (size_t r = 0; r < ds.size(); ++r) L.dst_off[r] = ds[r];
+            rc = mg_prepare(c, cf, ds.size(), M.K, L);
+            if (rc != MEC_OK) return rc;
+            HIP_TRY(launch_gf8_mg(L, st));
+            return MEC_OK;
+        }
         for (size_t r0 = 0; r0 < ds.size(); r0 += kMaxRows) {
             const int nr = int(std::min<size_t>(kMaxRows, ds.size() - r0));
             if (c->byte_wise()) {

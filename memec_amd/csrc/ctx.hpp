@@ -261,6 +261,12 @@ struct Layout {
 };
 
 void bit_block(const Field &f, unsigned e, uint32_t w, uint8_t *mask, size_t mstride);
+// A one-pass launch (gf8_mg_kernel) of coef (nd x ns, nd > 4, GF(2^8)):
+// structure, rows per group and the device copy of its tables into L.
+int mg_prepare(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, Gf8MgLaunch &L);
+// Byte-wise outputs beyond 4 per launch go through gf8_mg_kernel (every
+// source read once) unless MEC_WIDE=0 or the chunk has a sub-16-byte tail.
+bool mg_wanted(const mec_ctx *c, size_t nd);
 // outputs (^)= coef (nd x ns over GF(2^w)) * sources, every stripe.
 int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bool accumulate, hipStream_t stream);
 int apply(mec_ctx *c, const uint8_t *src, int64_t sss, const std::vector<int64_t> &src_off, uint8_t *dst,

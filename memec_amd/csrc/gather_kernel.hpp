@@ -40,13 +40,6 @@ __device__ __forceinline__ uint32_t gather_desc(const GatherParams &p, uint32_t 
     return p.pat ? uint32_t(p.pat[s]) : 0u;
 }
 
-// Uniform 64-bit / 32-bit values read back from LDS into SGPRs.
-__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v));
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
-    return uint64_t(hi) << 32 | lo;
-}
-__device__ __forceinline__ uint32_t uniform32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // Block prologue of both gathered kernels, three dependent latencies: the
 // stripe's descriptor index; the descriptor's first NDW dwords, one dword

@@ -216,18 +216,24 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
 // store).  S = kGf8Vand: group 0 has row 0 and column 0 all ones, the others
 // column 0 (Jerasure / ISA-L RS parity rows); kGf8Dense otherwise.  One-wave
 // blocks, strided layouts only (pointer batches split rows in groups of 4).
+// G = gather (pointer batches with one map for every stripe): source j /
+// output r of stripe s are the chunk pointers stab[s * sstride + src_off[j]]
+// / dtab[s * dstride + dst_off[r]] (as gf8_kernel's gather mode).
 template <int K>
 struct Gf8MgParams {
     const uint8_t *src;
     uint8_t *dst;
     int64_t sss, dss;
+    const uint64_t *stab, *dtab;
+    uint64_t s0;
+    uint32_t sstride, dstride;
     const uint32_t *tabs;  // device: groups x R x K x 8 dwords
     uint32_t chunk, units, tiles, accumulate, win, nstr, sgroup, srun, groups, pad;
     int64_t src_off[K];
     int64_t dst_off[kMaxSrc];  // groups x R rows; < 0 = padding
 };
 
-template <int K, int R, int S>
+template <int K, int R, int S, bool G>
 __global__ __launch_bounds__(kWaveBlock) void gf8_mg_kernel(const Gf8MgParams<K> p) {
     extern __shared__ uint32_t mtab[];
     const uint32_t ntab = p.groups * R * K * 8;
@@ -239,18 +245,22 @@ __global__ __launch_bounds__(kWaveBlock) void gf8_mg_kernel(const Gf8MgParams<K>
     const uint32_t u = tile * kWaveBlock + threadIdx.x;
     if (u >= p.units) return;
     const uint32_t off = u * 16;
+    const uint64_t gs = p.s0 + stripe;
     u32x4 d[K];
 #pragma unroll
-    for (int j = 0; j < K; ++j)
-        d[j] = buf_ld<u32x4>(chunk_rsrc(uint64_t(uintptr_t(p.src + int64_t(stripe) * p.sss + p.src_off[j])), p.chunk),
-                             off, true);
-    uint8_t *db = p.dst + int64_t(stripe) * p.dss;
+    for (int j = 0; j < K; ++j) {
+        const uint64_t a = G ? uniform64(p.stab[gs * p.sstride + p.src_off[j]])
+                             : uint64_t(uintptr_t(p.src + int64_t(stripe) * p.sss + p.src_off[j]));
+        d[j] = buf_ld<u32x4>(chunk_rsrc(a, p.chunk), off, true);
+    }
+    uint8_t *db = G ? nullptr : p.dst + int64_t(stripe) * p.dss;
     auto group = [&](uint32_t g, auto apply) {
         __amdgpu_buffer_rsrc_t dr[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
             const int64_t o = p.dst_off[g * R + i];
-            dr[i] = chunk_rsrc(o < 0 ? 0 : uint64_t(uintptr_t(db + o)), p.chunk);
+            const uint64_t a = o < 0 ? 0 : G ? uniform64(p.dtab[gs * p.dstride + uint64_t(o)]) : uint64_t(uintptr_t(db + o));
+            dr[i] = chunk_rsrc(a, p.chunk);
         }
         u32x4 acc[R];
 #pragma unroll
@@ -388,6 +398,11 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
     p.sss = L.src_stripe_stride;
     p.dss = L.dst_stripe_stride;
     p.tabs = L.tabs;
+    p.stab = L.stab;
+    p.dtab = L.dtab;
+    p.sstride = L.sstride;
+    p.dstride = L.dstride;
+    p.s0 = 0;
     p.chunk = uint32_t(L.len);
     const Geometry g = geometry(L.len / 16, kWaveBlock);
     p.units = g.units;
@@ -401,11 +416,21 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
     if (g.units == 0) return hipSuccess;
     for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
         const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-        p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-        p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-        p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
-        p.nstr = ns;
-        p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
+        if (L.stab) {  // pointer rows: no layout to window or group over
+            p.src = nullptr;
+            p.dst = nullptr;
+            p.s0 = s0;
+            p.win = 1;
+            p.nstr = 0;
+            p.sgroup = 0;
+            p.srun = 8;
+        } else {
+            p.src = L.src + int64_t(s0) * L.src_stripe_stride;
+            p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+            p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
+            p.nstr = ns;
+            p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
+        }
         // the tables are the block's LDS, and no wave cap: the caps of the
         // <= 4-row launches (gf8_target_waves) starve these longer-computing
         // waves — uncapped, RS(10,6)@256 KiB 67.2 -> 72.3 %, RS(8,5)@16 KiB
@@ -414,10 +439,17 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
         // still forces one (experiments)
         const uint32_t cap = occupancy_lds(kWaveBlock, kWaveBlock, 0, 0);
         const uint32_t lds = std::max(cap, tab_bytes);
-        if (L.vand)
-            hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Vand>), dim3(ns * g.tiles), dim3(kWaveBlock), lds, stream, p);
-        else
-            hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Dense>), dim3(ns * g.tiles), dim3(kWaveBlock), lds, stream, p);
+        const dim3 grid(ns * g.tiles), block(kWaveBlock);
+        if (L.stab) {
+            if (L.vand)
+                hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Vand, true>), grid, block, lds, stream, p);
+            else
+                hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Dense, true>), grid, block, lds, stream, p);
+        } else if (L.vand) {
+            hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Vand, false>), grid, block, lds, stream, p);
+        } else {
+            hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Dense, false>), grid, block, lds, stream, p);
+        }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

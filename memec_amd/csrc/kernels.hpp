@@ -115,6 +115,11 @@ struct Gf8MgLaunch {
     const uint8_t *src;
     uint8_t *dst;
     int64_t src_stripe_stride, dst_stripe_stride;
+    // pointer batches (one map for every stripe): chunk pointers at
+    // stab[s * sstride + src_off[j]], dtab[s * dstride + dst_off[r]]
+    // (device-readable); src / dst unused then
+    const uint64_t *stab, *dtab;
+    uint32_t sstride, dstride;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[kMaxSrc];
     int k, rows, group_rows;

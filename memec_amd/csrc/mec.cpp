@@ -73,6 +73,23 @@ int mg_tables(mec_ctx *c, const Mat &coef, size_t rows, size_t ns, int R, const 
     return MEC_OK;
 }
 
+int mg_prepare(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, Gf8MgLaunch &L) {
+    bool vand = true;  // row 0 and column 0 all ones (Jerasure / ISA-L RS parity rows)
+    for (size_t j = 0; j < ns && vand; ++j) vand = coef[j] == 1;
+    for (size_t r = 0; r < nd && vand; ++r) vand = coef[r * ns] == 1;
+    L.vand = vand;
+    L.group_rows = mec::gf8_mg_rows(int(nd), int(ns), vand);
+    const int64_t kr = mec::detail::knob(mec::detail::kKnobMgRows);  // experiments (mec_set_knob)
+    if (kr == 3 || kr == 4 || (kr == 8 && ns >= size_t(mec::kMg8MinK) && ns <= size_t(mec::kMg8MaxK)))
+        L.group_rows = int(kr);
+    return mg_tables(c, coef, nd, ns, L.group_rows, L.tabs);
+}
+
+bool mg_wanted(const mec_ctx *c, size_t nd) {
+    return c->byte_wise() && nd > size_t(mec::kMaxRows) && c->cs % 16 == 0 &&
+           mec::detail::knob(mec::detail::kKnobWide) != 0;
+}
+
 // outputs (^)= coef (nd x ns over GF(2^w)) * sources, every stripe.
 int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bool accumulate, hipStream_t stream) {
     const size_t ns = lay.ns, nd = lay.nd;
@@ -85,8 +102,7 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
         return MEC_OK;
     }
     const bool probe = c->probe.load(std::memory_order_relaxed) == MEC_PROBE_XOR;
-    if (c->byte_wise() && nd > size_t(mec::kMaxRows) && c->cs % 16 == 0 && !probe &&
-        mec::detail::knob(mec::detail::kKnobWide) != 0) {
+    if (mg_wanted(c, nd) && !probe) {
         // more than 4 outputs: one pass over the sources (gf8_mg_kernel)
         mec::Gf8MgLaunch L{};
         L.src = lay.src;
@@ -100,15 +116,7 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
         L.accumulate = accumulate;
         for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
         for (size_t r = 0; r < nd; ++r) L.dst_off[r] = lay.dst_off[r];
-        bool vand = true;  // row 0 and column 0 all ones (Jerasure / ISA-L RS parity rows)
-        for (size_t j = 0; j < ns && vand; ++j) vand = coef[j] == 1;
-        for (size_t r = 0; r < nd && vand; ++r) vand = coef[r * ns] == 1;
-        L.vand = vand;
-        L.group_rows = mec::gf8_mg_rows(int(nd), int(ns), vand);
-        const int64_t kr = mec::detail::knob(mec::detail::kKnobMgRows);  // experiments (mec_set_knob)
-        if (kr == 3 || kr == 4 || (kr == 8 && ns >= size_t(mec::kMg8MinK) && ns <= size_t(mec::kMg8MaxK)))
-            L.group_rows = int(kr);
-        int rc = mg_tables(c, coef, nd, ns, L.group_rows, L.tabs);
+        int rc = mg_prepare(c, coef, nd, ns, L);
         if (rc != MEC_OK) return rc;
         HIP_TRY(mec::launch_gf8_mg(L, stream));
         return MEC_OK;

@@ -140,6 +140,14 @@ uint32_t bm_windows(const void *src, int64_t src_span, const void *dst, int64_t 
     X(17, R) X(18, R) X(19, R) X(20, R) X(21, R) X(22, R) X(23, R) X(24, R) X(25, R) X(26, R) X(27, R) X(28, R) X(29, R) X(30, R) X(31, R)
 #define MEC_FOR_K(X, R) MEC_FOR_K_LO(X, R) MEC_FOR_K_HI(X, R)
 
+// Uniform 64-bit / 32-bit values (read back from LDS or memory) into SGPRs.
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(uint32_t(v));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(uint32_t(v >> 32));
+    return uint64_t(hi) << 32 | lo;
+}
+__device__ __forceinline__ uint32_t uniform32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
 // ---------------------------------------------------------------------------
 // partial (tail) units: < 16 bytes at the end of a region
 // ---------------------------------------------------------------------------

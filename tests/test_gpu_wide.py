@@ -259,3 +259,56 @@ def test_wide_decode_batch_mixed_patterns(fam, mem):
         for i in range(k + m):
             assert np.array_equal(chunk_of(after, slab, row[i]), chunks[i]), (fam, mem, s, pats[s], i)
     c.close()
+
+
+@pytest.mark.parametrize("mem", ["device", "host"])
+@pytest.mark.parametrize("fam", ["rs", "isal_rs", "isal_cauchy"])
+def test_wide_batch_one_map_one_pass(fam, mem):
+    """Pointer batches whose stripes share one map (every parity wanted, no
+    zero columns; one erasure pattern): the one-pass kernel reads the
+    pointer rows itself (gathered gf8_mg_kernel: row-0 / column-0 XORs,
+    groups of 8 at K = 16, of 3 + 3 at K = 6), scattered 8-byte-aligned
+    slots: encode, then in-place decode of the same 6 erasures in every
+    stripe."""
+    for k, m, cs, n in [(16, 8, 4096, 20), (6, 6, 2048, 24)]:
+        rng = np.random.default_rng(k * 31 + m)
+        slots = rng.permutation(n * (k + m))
+        slab = Slab(n * (k + m), cs, 8, mem == "device", 500 + k)
+        before = slab.snapshot()
+        c = Codec(fam, k, m, cs)
+        dptr, pptr = [], []
+        for s in range(n):
+            row = slots[s * (k + m):(s + 1) * (k + m)]
+            dptr += [slab.addr(row[j]) for j in range(k)]
+            pptr += [slab.addr(row[k + i]) for i in range(m)]
+        c.encode_batch(dptr, pptr, mem=mem)
+        after = slab.snapshot()
+        full = []
+        for s in range(n):
+            row = slots[s * (k + m):(s + 1) * (k + m)]
+            data = [chunk_of(before, slab, row[j]).copy() for j in range(k)]
+            par = O.encode(fam, k, m, data, cs)
+            for i in range(m):
+                assert np.array_equal(chunk_of(after, slab, row[k + i]), par[i]), (fam, mem, k, m, s, i)
+            full.append(data + list(par))
+        # the same 6 erasures in every stripe, rebuilt in place
+        pat = [0, 2, 5, k, k + 1, k + m - 1]
+        present = sum(1 << i for i in range(k + m) if i not in pat)
+        ptrs = []
+        for s in range(n):
+            row = slots[s * (k + m):(s + 1) * (k + m)]
+            ptrs += [slab.addr(i) for i in row]
+            for i in pat:
+                o = int(row[i]) * slab.slot + slab.hdr
+                if slab.t is not None:
+                    slab.t[o:o + cs] = 0
+                else:
+                    slab.host[o:o + cs] = 0
+        res = c.decode_batch(ptrs, [present] * n, mem=mem)
+        assert all(r == 0 for r in res), res
+        after = slab.snapshot()
+        for s in range(n):
+            row = slots[s * (k + m):(s + 1) * (k + m)]
+            for i in range(k + m):
+                assert np.array_equal(chunk_of(after, slab, row[i]), full[s][i]), (fam, mem, k, m, s, i)
+        c.close()
