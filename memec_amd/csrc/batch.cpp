@@ -309,7 +309,9 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
     // the pointer rows itself, with the map's tables and structure (row 0 /
     // column 0 XORs, groups of 3, 4 or 8) like a strided launch
     const bool one_pass = one_map && M.K >= 1 && mg_wanted(c, M.rows());
-    const bool single = one_map && (M.rows() <= size_t(kMaxRows) || one_pass);
+    // (bitmatrix maps: up to 8 outputs per gathered bm_kernel launch)
+    const bool single =
+        one_map && (M.rows() <= size_t(c->byte_wise() ? kMaxRows : kMaxBmOut) || one_pass);
     std::vector<uint32_t> descs;
     uint32_t desc_dw = 0;
     const size_t groups = single ? 0 : build_descs(c, M, descs, desc_dw);
@@ -351,8 +353,9 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
             HIP_TRY(launch_gf8_mg(L, st));
             return MEC_OK;
         }
-        for (size_t r0 = 0; r0 < ds.size(); r0 += kMaxRows) {
-            const int nr = int(std::min<size_t>(kMaxRows, ds.size() - r0));
+        const size_t step = c->byte_wise() ? size_t(kMaxRows) : size_t(kMaxBmOut);
+        for (size_t r0 = 0; r0 < ds.size(); r0 += step) {
+            const int nr = int(std::min<size_t>(step, ds.size() - r0));
             if (c->byte_wise()) {
                 Gf8Launch L{};
                 L.stab = dstab;

@@ -205,7 +205,7 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
             const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
             if (L.stab) {
                 p.s0 = s0;
-                if constexpr (VW == bm_vw<W>() && R <= kMaxRows) {
+                if constexpr (VW == bm_vw<W>()) {
                     const uint32_t glds = gathered_lds(bt, 0, gshape);
                     if (bt == kWaveBlock)
                         hipLaunchKernelGGL((bm_kernel<W, R, true, kWaveBlock>), dim3(ns * g.tiles), dim3(bt), glds, stream, p);

@@ -525,7 +525,7 @@ void gf8_mg_tables(const uint8_t *coef, int rows, int k, int R, std::vector<uint
 }
 
 hipError_t launch_bm(const BmLaunch &L, hipStream_t stream) {
-    if (L.k < 1 || L.k > kMaxK || L.rows < 1 || L.rows > (L.stab ? kMaxRows : kMaxBmOut) || L.w < 1 || L.w > 8)
+    if (L.k < 1 || L.k > kMaxK || L.rows < 1 || L.rows > kMaxBmOut || L.w < 1 || L.w > 8)
         return hipErrorInvalidValue;
     if (L.packet == 0 || L.n_stripes == 0) return hipSuccess;
     return kBmTable[size_t(L.w - 1) * kMaxBmOut + size_t(L.rows - 1)](L, stream);

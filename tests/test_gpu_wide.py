@@ -262,15 +262,18 @@ def test_wide_decode_batch_mixed_patterns(fam, mem):
 
 
 @pytest.mark.parametrize("mem", ["device", "host"])
-@pytest.mark.parametrize("fam", ["rs", "isal_rs", "isal_cauchy"])
+@pytest.mark.parametrize("fam", ["rs", "isal_rs", "isal_cauchy", "cauchy"])
 def test_wide_batch_one_map_one_pass(fam, mem):
     """Pointer batches whose stripes share one map (every parity wanted, no
     zero columns; one erasure pattern): the one-pass kernel reads the
     pointer rows itself (gathered gf8_mg_kernel: row-0 / column-0 XORs,
     groups of 8 at K = 16, of 3 + 3 at K = 6), scattered 8-byte-aligned
     slots: encode, then in-place decode of the same 6 erasures in every
-    stripe."""
-    for k, m, cs, n in [(16, 8, 4096, 20), (6, 6, 2048, 24)]:
+    stripe.  Cauchy bitmatrix maps of up to 8 outputs run one gathered
+    bm_kernel launch."""
+    for k, m, cs, n in [(16, 8, 4096, 20), (6, 6, 2048, 24), (10, 6, 4096, 12)]:
+        if not ok_shape(fam, k, m, cs):
+            continue
         rng = np.random.default_rng(k * 31 + m)
         slots = rng.permutation(n * (k + m))
         slab = Slab(n * (k + m), cs, 8, mem == "device", 500 + k)
