@@ -79,7 +79,7 @@
 extern "C" {
 #endif
 
-#define MEC_ABI_VERSION 4
+#define MEC_ABI_VERSION 5
 #define MEC_MAX_CHUNKS 32 /* k + m <= 32: RS_N_MAX / CRS_N_MAX (rscoding.hh:5, cauchycoding.hh:5) */
 
 typedef enum {
@@ -119,6 +119,12 @@ typedef struct {
     uint32_t queue_broken;       /* 1: a call timed out and the queue stopped for good */
     uint32_t queue_devslot;      /* 1: slot descriptors in device memory, written through the BAR */
     uint64_t queue_timeouts;     /* calls that hit MEC_QUEUE_TIMEOUT_MS */
+    /* one-pass (> 4 output) permute tables: device bytes held, matrices
+     * cached, and launches that ran as 4-row groups because the cache was at
+     * its cap (MEC_MG_CACHE_BYTES at mec_create, default 64 MiB; ABI 5) */
+    uint64_t mg_cache_bytes;
+    uint64_t mg_cache_tables;
+    uint64_t mg_cache_uncached;
 } mec_stats;
 
 typedef struct {
@@ -139,6 +145,13 @@ int mec_abi_version(void);
  * MEC_EINVAL where the reference would exit(-1). */
 int mec_create(int family, uint32_t k, uint32_t m, uint32_t chunk_size, int device,
                mec_ctx **out);
+/* Frees the context.  With a host queue (mec_set_host_queue) the resident
+ * kernel is stopped first; if it does not leave within max(timeout, 1 s) —
+ * a job that never completes — its memory and the context's staging lanes
+ * are leaked rather than freed under it, a message goes to stderr, and
+ * mec_destroy returns while that kernel may still read the job's source
+ * chunks and write its outputs: the caller must keep registered chunks of
+ * a call that failed with MEC_EHIP alive. */
 void mec_destroy(mec_ctx *ctx);
 /* Thread-local description of the last failure on this thread. */
 const char *mec_last_error(void);

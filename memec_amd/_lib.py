@@ -8,7 +8,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libmec.so")
+# MEMEC_LIBMEC: another build of the same library (the bounds-checked
+# debug build, make -C memec_amd bounds); default the in-tree release build
+LIB_PATH = os.environ.get("MEMEC_LIBMEC") or os.path.join(HERE, "libmec.so")
 
 MEC_OK, MEC_EINVAL, MEC_ENOMEM, MEC_EHIP, MEC_ETOOMANY, MEC_ESINGULAR, MEC_ENODEV = 0, -1, -2, -3, -4, -5, -6
 FAMILIES = {"rs": 0, "cauchy": 1, "isal_rs": 2, "isal_cauchy": 3}
@@ -43,7 +45,8 @@ class MecStats(ctypes.Structure):
                 ("staged_calls", ctypes.c_uint64), ("queue_calls", ctypes.c_uint64),
                 ("queue_launches", ctypes.c_uint64), ("queue_slots", ctypes.c_uint32),
                 ("queue_parts", ctypes.c_uint32), ("queue_broken", ctypes.c_uint32), ("queue_devslot", ctypes.c_uint32),
-                ("queue_timeouts", ctypes.c_uint64)]
+                ("queue_timeouts", ctypes.c_uint64), ("mg_cache_bytes", ctypes.c_uint64),
+                ("mg_cache_tables", ctypes.c_uint64), ("mg_cache_uncached", ctypes.c_uint64)]
 
 
 _lib = None

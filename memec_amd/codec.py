@@ -212,7 +212,8 @@ class Codec:
                 "staged_calls": st.staged_calls, "queue_calls": st.queue_calls,
                 "queue_launches": st.queue_launches, "queue_slots": st.queue_slots,
                 "queue_parts": st.queue_parts, "queue_broken": bool(st.queue_broken), "queue_devslot": bool(st.queue_devslot),
-                "queue_timeouts": st.queue_timeouts}
+                "queue_timeouts": st.queue_timeouts, "mg_cache_bytes": st.mg_cache_bytes,
+                "mg_cache_tables": st.mg_cache_tables, "mg_cache_uncached": st.mg_cache_uncached}
 
 
 def fill_random(t, seed, word_offset=0, stream=None):

@@ -348,10 +348,13 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
             L.accumulate = M.accumulate;
             for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
             for (size_t r = 0; r < ds.size(); ++r) L.dst_off[r] = ds[r];
-            rc = mg_prepare(c, cf, ds.size(), M.K, L);
-            if (rc != MEC_OK) return rc;
-            HIP_TRY(launch_gf8_mg(L, st));
-            return MEC_OK;
+            rc = mg_prepare(c, cf, ds.size(), M.K, L, st);
+            if (rc == MEC_OK) {
+                HIP_TRY(launch_gf8_mg(L, st));
+                return MEC_OK;
+            }
+            if (rc != kMgUncached) return rc;
+            // past the table cache's cap: 4-row launches below
         }
         const size_t step = c->byte_wise() ? size_t(kMaxRows) : size_t(kMaxBmOut);
         for (size_t r0 = 0; r0 < ds.size(); r0 += step) {
@@ -966,6 +969,12 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
         std::lock_guard<std::mutex> pk(c->plan_mu);
         out->cached_plans = c->plans.size();
     }
+    {
+        std::lock_guard<std::mutex> mk(c->mg.mu);
+        out->mg_cache_bytes = c->mg.bytes;
+        out->mg_cache_tables = c->mg.map.size();
+        out->mg_cache_uncached = c->mg.uncached;
+    }
     for (mec_ctx *sc : c->shards) {  // a multi context reports its shards' sums
         mec_stats t{};
         (void)mec_get_stats(sc, &t);
@@ -981,6 +990,9 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
         out->queue_broken |= t.queue_broken;
         out->queue_devslot |= t.queue_devslot;
         out->queue_timeouts += t.queue_timeouts;
+        out->mg_cache_bytes += t.mg_cache_bytes;
+        out->mg_cache_tables += t.mg_cache_tables;
+        out->mg_cache_uncached += t.mg_cache_uncached;
     }
     return MEC_OK;
 }

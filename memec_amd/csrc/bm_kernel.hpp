@@ -169,84 +169,52 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
     p.sstride = L.sstride;
     p.dstride = L.dstride;
     p.chunk = uint32_t(L.packet * uint64_t(L.w));
-    p.s0 = 0;
-    // block size from the whole launch's layout (sub-launches share it)
-    // gathered: aligned chunks keep the default shape (one-wave blocks cost
-    // the bitmatrix kernel 3.5 % on aligned decode batches), unaligned ones
-    // take the capped 4-wave shape (+1-3 %; profiles/r02/host/gather_ab_bm.log)
-    const uint8_t gshape = L.gshape == 1 ? 0 : L.gshape;
-    // one-wave blocks in place: chunks of kBmWaveChunk or more, and
-    // 16-32 KiB chunks with <= 2 output rows and k >= 6 (8-byte lanes, 12
-    // waves per CU; CRS(6,2) / (8,2) / (12,2) in place +1-5 points,
-    // CRS(4,2), CRS(12,4), 8 KiB and >= 64 KiB chunks lose;
-    // profiles/r02/bmshape/)
-    const uint64_t cb = uint64_t(p.chunk);
-    const bool wave_ip = cb >= kBmWaveChunk || (R <= 2 && L.k >= 6 && cb >= (16u << 10) && cb <= (32u << 10));
-    const uint32_t bt = L.stab ? gathered_block_threads(gshape)
-                               : block_threads(true, bm_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
-                                                                int64_t(L.n_stripes) * L.dst_stripe_stride, cb, R, L.k),
-                                               wave_ip);
-    const Geometry g = geometry(L.packet / UB, bt);
-    p.units = g.units;
-    p.tiles = g.tiles;
     p.accumulate = L.accumulate ? 1u : 0u;
-    p.win = 1;
     p.pad = 0;
-    p.nstr = 0;
-    p.sgroup = 0;
-    p.srun = 8;
     p.pad2 = 0;
     for (int j = 0; j < kMaxSrc; ++j) p.src_off[j] = j < L.k ? L.src_off[j] : 0;
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int j = 0; j < kMaxSrc; ++j)
         for (int r = 0; r < R * W; ++r) p.mask[j][r] = j < L.k ? L.mask[j][r] : 0;
-    if (g.units > 0) {
-        for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
-            const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-            if (L.stab) {
-                p.s0 = s0;
-                if constexpr (VW == bm_vw<W>()) {
-                    const uint32_t glds = gathered_lds(bt, 0, gshape);
-                    if (bt == kWaveBlock)
-                        hipLaunchKernelGGL((bm_kernel<W, R, true, kWaveBlock>), dim3(ns * g.tiles), dim3(bt), glds, stream, p);
-                    else
-                        hipLaunchKernelGGL((bm_kernel<W, R, true, kThreads>), dim3(ns * g.tiles), dim3(bt), glds, stream, p);
-                } else {
-                    return hipErrorInvalidValue;  // gathered launches use the default lane width
-                }
-            } else {
-                p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-                p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-                p.win = bm_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride, cb, R,
-                                   L.k);
-                p.nstr = ns;
-                p.sgroup = stripe_group(p.chunk, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, true, p.srun);
-                const bool in_place = p.win > 1;
-                const uint32_t lds = occupancy_lds(bt, std::min<uint32_t>(bt, g.units), 0, bm_target_waves(R, W, VW, in_place));
-                if (bt == kWaveBlock)
-                    hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock, VW>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
-                else
-                    hipLaunchKernelGGL((bm_kernel<W, R, false, kThreads, VW>), dim3(ns * g.tiles), dim3(bt), lds, stream, p);
-            }
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
+    for (uint32_t s0 = 0; s0 < L.n_stripes;) {
+        const KernelPlan pl = plan_bm(L, s0);
+        if (!pl.ok || pl.k != L.k || pl.rows != R || pl.vw != uint32_t(VW)) return hipErrorInvalidValue;
+        if (pl.geo.units == 0) break;
+        p.units = pl.geo.units;
+        p.tiles = pl.geo.tiles;
+        p.s0 = s0;
+        p.win = pl.win;
+        p.nstr = L.stab ? 0 : pl.ns;
+        p.sgroup = pl.sgroup;
+        p.srun = pl.srun;
+        p.src = L.stab ? nullptr : L.src + int64_t(s0) * L.src_stripe_stride;
+        p.dst = L.stab ? nullptr : L.dst + int64_t(s0) * L.dst_stripe_stride;
+        const dim3 grid(uint32_t(pl.grid)), block(pl.bt);
+        if (L.stab) {
+            if (pl.bt == kWaveBlock)
+                hipLaunchKernelGGL((bm_kernel<W, R, true, kWaveBlock, VW>), grid, block, pl.lds_dynamic, stream, p);
+            else
+                hipLaunchKernelGGL((bm_kernel<W, R, true, kThreads, VW>), grid, block, pl.lds_dynamic, stream, p);
+        } else {
+            if (pl.bt == kWaveBlock)
+                hipLaunchKernelGGL((bm_kernel<W, R, false, kWaveBlock, VW>), grid, block, pl.lds_dynamic, stream, p);
+            else
+                hipLaunchKernelGGL((bm_kernel<W, R, false, kThreads, VW>), grid, block, pl.lds_dynamic, stream, p);
         }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        s0 += pl.ns;
     }
-    if (L.packet % UB) return launch_bm_tail(L, uint64_t(g.units) * UB, stream);
+    if (L.packet % UB) return launch_bm_tail(L, uint64_t(L.packet / UB) * UB, stream);
     return hipSuccess;
 }
 
-// Lane width of a strided launch (bm_lane_bytes); gathered launches keep
-// the default width.
+// Lane width from the plan (bm_lane_bytes for strided launches; gathered
+// launches keep the default width).
 template <int W, int R>
 hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
     if constexpr (bm_vw<W>() == 4) {
-        if (!L.stab) {
-            const bool in_place = bm_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
-                                             int64_t(L.n_stripes) * L.dst_stripe_stride, L.packet * uint64_t(L.w), R,
-                                             L.k) > 1;
-            if (bm_lane_bytes(W, R, L.packet * uint64_t(L.w), in_place) == 8) return run_bm_vw<W, R, 2>(L, stream);
-        }
+        if (L.n_stripes && plan_bm(L, 0).vw == 2) return run_bm_vw<W, R, 2>(L, stream);
     }
     return run_bm_vw<W, R, bm_vw<W>()>(L, stream);
 }
@@ -256,7 +224,7 @@ hipError_t run_bm(const BmLaunch &L, hipStream_t stream) {
 #define MEC_FOR_R4(X, W) X(W, 1) X(W, 2) X(W, 3) X(W, 4)
 #define MEC_FOR_R8(X, W) MEC_FOR_R4(X, W) X(W, 5) X(W, 6) X(W, 7) X(W, 8)
 #define MEC_FOR_W(F, X) F(X, 1) F(X, 2) F(X, 3) F(X, 4) F(X, 5) F(X, 6) F(X, 7) F(X, 8)
-// strided launches take up to kMaxBmOut outputs (R = 1..8), gathered ones 4
+// strided and gathered launches take up to kMaxBmOut = 8 outputs (R = 1..8)
 #define MEC_BM_INSTANTIATE_W(W) MEC_FOR_R8(MEC_BM_ONE, W)
 
 }  // namespace detail

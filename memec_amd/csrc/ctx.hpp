@@ -149,6 +149,30 @@ struct alignas(256) QDevSlot {
     uint64_t pad0[7];
     QDesc d;
 };
+// The one-pass kernel's permute tables (gf8_mg_kernel), one entry per
+// distinct > 4-row matrix: suballocated from device arena blocks with a
+// pinned host mirror (the image stays there as the source of its async
+// upload), uploaded on the calling stream; `ready` fires when the upload
+// has landed, so a hit from another stream waits for it on the device.
+// At most `cap` bytes: matrices past it (a decode that walks through many
+// erasure patterns) run as 4-row launches with their coefficients in
+// kernel arguments instead of growing the cache.
+struct MgEntry {
+    const uint32_t *dev = nullptr;
+    hipEvent_t ready = nullptr;
+    bool landed = false;
+};
+struct MgCache {
+    std::mutex mu;
+    std::unordered_map<std::string, MgEntry> map;
+    std::vector<uint8_t *> dev_blocks, host_blocks;
+    size_t block_used = 0;   // bytes used in the last block
+    size_t bytes = 0;        // bytes handed to entries
+    size_t cap = 0;          // MEC_MG_CACHE_BYTES at mec_create (default 64 MiB)
+    uint64_t uncached = 0;   // launches that fell back past the cap
+};
+constexpr size_t kMgBlock = size_t(4) << 20;
+
 // Grid-wide control words, after the slots in the same mapped allocation.
 enum : uint32_t { kQCtlStop = 0, kQCtlExit = 1, kQCtlWords = 2 };
 struct HostQueue {
@@ -209,9 +233,9 @@ struct mec_ctx {
     // arithmetic-free twin (measurement only)
     std::atomic<int> probe{0};
     // device copies of the permute tables of > 4-row matrices
-    // (gf8_mg_kernel), keyed by (rows, k, coefficient bytes); uploaded once
-    std::mutex mg_mu;
-    std::unordered_map<std::string, uint32_t *> mg_tabs;
+    // (gf8_mg_kernel), keyed by (rows, k, rows per group, coefficient
+    // bytes); bounded (mec.cpp mg_tables)
+    mec::core::MgCache mg;
 
     bool byte_wise() const { return family != MEC_CAUCHY_GOOD; }
     mec::Scheme scheme() const {
@@ -263,7 +287,11 @@ struct Layout {
 void bit_block(const Field &f, unsigned e, uint32_t w, uint8_t *mask, size_t mstride);
 // A one-pass launch (gf8_mg_kernel) of coef (nd x ns, nd > 4, GF(2^8)):
 // structure, rows per group and the device copy of its tables into L.
-int mg_prepare(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, Gf8MgLaunch &L);
+// MEC_OK, kMgUncached (the cache is full: the caller codes the rows in
+// groups of 4 instead) or an error.
+constexpr int kMgUncached = 1;
+int mg_prepare(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, Gf8MgLaunch &L, hipStream_t stream);
+void mg_release(mec_ctx *c);
 // Byte-wise outputs beyond 4 per launch go through gf8_mg_kernel (every
 // source read once) unless MEC_WIDE=0 or the chunk has a sub-16-byte tail.
 bool mg_wanted(const mec_ctx *c, size_t nd);
@@ -314,7 +342,10 @@ hipError_t lane_sync(hipStream_t s);
 // eligible, no free slot, or a timed-out job that was withdrawn (nothing
 // done: the caller takes the launch path), else rc holds the result.
 bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Mat &coef, bool accumulate, int &rc);
-void queue_stop(mec_ctx *c);
+// Stop the resident kernel and free the queue; false if the grid was still
+// running at the drain cap (the queue's memory is then leaked, and so must
+// be anything its jobs can address: mec_destroy keeps the staging lanes).
+bool queue_stop(mec_ctx *c);
 
 // batch.cpp
 void batch_release(mec_ctx *c);  // frees table slots and the host pipeline

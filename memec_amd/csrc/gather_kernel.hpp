@@ -50,6 +50,7 @@ __device__ __forceinline__ bool gather_prologue(const GatherParams &p, uint32_t 
                                                 uint64_t *ptr, int sel_dw, int dsel_dw) {
     const uint32_t di = gather_desc(p, s);
     if (di == kSkipStripe) return false;
+    MEC_DASSERT(p.group_maps == 0 || di < p.group_maps);
     const uint32_t *D = p.desc + size_t(di) * p.desc_dw;
     constexpr int NI = (NDW + kThreads - 1) / kThreads;
     uint32_t v[NI];
@@ -67,9 +68,11 @@ __device__ __forceinline__ bool gather_prologue(const GatherParams &p, uint32_t 
     const int t = threadIdx.x;
     if (t < int(k)) {
         const uint32_t sel = (dsc[sel_dw + t / 4] >> (8 * (t % 4))) & 0xffu;
+        MEC_DASSERT(sel < p.sstride);
         ptr[t] = p.stab[uint64_t(s) * p.sstride + sel];
     } else if (t >= 64 && t < 64 + R) {
         const uint32_t sel = (dsc[dsel_dw + (t - 64) / 4] >> (8 * ((t - 64) % 4))) & 0xffu;
+        MEC_DASSERT(sel == kNoRow || sel < p.dstride);
         ptr[KMAX + t - 64] = sel == kNoRow ? 0 : p.dtab[uint64_t(s) * p.dstride + sel];
     }
     __syncthreads();
@@ -131,6 +134,7 @@ __global__ __launch_bounds__(kThreads) void gf8_gather_kernel(const GatherParams
             __syncthreads();
             if (threadIdx.x < R) {
                 const uint32_t sel = (dsc[16] >> (8 * threadIdx.x)) & 0xffu;
+                MEC_DASSERT(sel == kNoRow || sel < p.dstride);
                 ptr[K + threadIdx.x] = sel == kNoRow ? 0 : p.dtab[uint64_t(s) * p.dstride + sel];
             }
             __syncthreads();
@@ -227,31 +231,33 @@ inline GatherParams gather_params(const GatherLaunch &L, const Geometry &g) {
 
 template <int K, int R>
 hipError_t run_gf8_gather(const GatherLaunch &L, hipStream_t stream) {
-    const Geometry g = geometry(L.len / 16);
-    GatherParams p = gather_params(L, g);
-    if (g.units > 0) {
-        for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
-            const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-            p.s0 = s0;
-            if constexpr (R == kMaxRows) {
-                if (p.groups > 1)
-                    hipLaunchKernelGGL((gf8_gather_kernel<K, R, true>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-                else
-                    hipLaunchKernelGGL((gf8_gather_kernel<K, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-            } else {
-                if (p.groups > 1) return hipErrorInvalidValue;  // multi-group launches run 4 rows per group
-                hipLaunchKernelGGL((gf8_gather_kernel<K, R, false>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-            }
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
+    uint32_t units = 0;
+    for (uint32_t s0 = 0; s0 < L.n_stripes;) {
+        const KernelPlan pl = plan_gf8_gather(L, s0);
+        if (!pl.ok || pl.k != K || pl.rows != R) return hipErrorInvalidValue;
+        units = pl.geo.units;
+        if (units == 0) break;
+        GatherParams p = gather_params(L, pl.geo);
+        p.s0 = s0;
+        const dim3 grid(uint32_t(pl.grid)), block(kThreads);
+        if constexpr (R == kMaxRows) {
+            if (p.groups > 1)
+                hipLaunchKernelGGL((gf8_gather_kernel<K, R, true>), grid, block, 0, stream, p);
+            else
+                hipLaunchKernelGGL((gf8_gather_kernel<K, R, false>), grid, block, 0, stream, p);
+        } else {
+            hipLaunchKernelGGL((gf8_gather_kernel<K, R, false>), grid, block, 0, stream, p);
         }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        s0 += pl.ns;
     }
     if (L.len % 16)  // the tail, one launch per row group
         for (uint32_t grp = 0; grp < std::max(1u, L.groups); ++grp) {
             GatherLaunch Lg = L;
             Lg.desc = static_cast<const uint8_t *>(L.desc) + size_t(grp) * L.group_maps * L.desc_dw * sizeof(uint32_t);
             Lg.groups = 1;
-            hipError_t e = launch_gather_tail(Lg, false, uint64_t(g.units) * 16, stream);
+            hipError_t e = launch_gather_tail(Lg, false, uint64_t(L.len / 16) * 16, stream);
             if (e != hipSuccess) return e;
         }
     return hipSuccess;
@@ -260,18 +266,18 @@ hipError_t run_gf8_gather(const GatherLaunch &L, hipStream_t stream) {
 template <int W, int R>
 hipError_t run_bm_gather(const GatherLaunch &L, hipStream_t stream) {
     constexpr int UB = 4 * bm_vw<W>();
-    const Geometry g = geometry(L.len / UB);
-    GatherParams p = gather_params(L, g);
-    if (g.units > 0) {
-        for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
-            const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-            p.s0 = s0;
-            hipLaunchKernelGGL((bm_gather_kernel<W, R>), dim3(ns * g.tiles), dim3(kThreads), 0, stream, p);
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
-        }
+    for (uint32_t s0 = 0; s0 < L.n_stripes;) {
+        const KernelPlan pl = plan_bm_gather(L, s0);
+        if (!pl.ok || pl.rows != R || pl.vw * 4 != uint32_t(UB)) return hipErrorInvalidValue;
+        if (pl.geo.units == 0) break;
+        GatherParams p = gather_params(L, pl.geo);
+        p.s0 = s0;
+        hipLaunchKernelGGL((bm_gather_kernel<W, R>), dim3(uint32_t(pl.grid)), dim3(kThreads), 0, stream, p);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        s0 += pl.ns;
     }
-    if (L.len % UB) return launch_gather_tail(L, true, uint64_t(g.units) * UB, stream);
+    if (L.len % UB) return launch_gather_tail(L, true, uint64_t(L.len / UB) * UB, stream);
     return hipSuccess;
 }
 

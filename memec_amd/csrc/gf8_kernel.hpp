@@ -61,7 +61,8 @@ __device__ __forceinline__ u32x4 xor3(const u32x4 &a, const u32x4 &b, const u32x
 }
 
 // Matrix structure a launch is specialised for (chosen on the host from the
-// coefficients, so the kernel has no data-dependent branches):
+// coefficients, so the kernel has no data-dependent branches; constants in
+// launch_plan.hpp):
 //   kGf8Dense — every coefficient through its permute tables (a 0 / 1
 //               coefficient's tables give 0 / x, so any matrix is exact);
 //   kGf8Vand  — row 0 and column 0 all ones (Jerasure's Vandermonde
@@ -73,10 +74,6 @@ __device__ __forceinline__ u32x4 xor3(const u32x4 &a, const u32x4 &b, const u32x
 //               outputs are not codes.
 //   kGf8Col0  — column 0 all ones only: the row groups after the first of a
 //               Vandermonde matrix with more than one group (gf8_mg_kernel).
-constexpr int kGf8Dense = 0;
-constexpr int kGf8Vand = 1;
-constexpr int kGf8Xor = 2;
-constexpr int kGf8Col0 = 3;
 
 // acc[i] ^= sum_j coef(i, j) * d[j] for one 16-byte unit.  TB = the LDS
 // permute tables (8 dwords per coefficient b = i*K + j: t0 t1 u0 u1 v).
@@ -140,15 +137,6 @@ __device__ __forceinline__ void gf8_apply(const u32x4 (&d)[K], u32x4 (&acc)[R], 
 #pragma unroll
     for (int i = 0; i < R; ++i)
         if (has[i]) acc[i] ^= pend[i];
-}
-
-// Host side: the structure a coefficient block qualifies for.
-inline int gf8_structure(const Gf8Coef (*coef)[kMaxSrc], int k, int rows) {
-    const uint32_t one = 0x03020100u;  // t0 of coefficient 1 (identity on bits 0-2)
-    bool vand = true;
-    for (int j = 0; j < k && vand; ++j) vand = coef[0][j].t0 == one;
-    for (int i = 0; i < rows && vand; ++i) vand = coef[i][0].t0 == one;
-    return vand ? kGf8Vand : kGf8Dense;
 }
 
 // G = gather: chunk addresses come from per-stripe pointer rows (the
@@ -237,6 +225,7 @@ template <int K, int R, int S, bool G>
 __global__ __launch_bounds__(kWaveBlock) void gf8_mg_kernel(const Gf8MgParams<K> p) {
     extern __shared__ uint32_t mtab[];
     const uint32_t ntab = p.groups * R * K * 8;
+    MEC_DASSERT(p.groups * R <= uint32_t(kMaxSrc));
     for (uint32_t t = threadIdx.x; t < ntab; t += kWaveBlock) mtab[t] = p.tabs[t];
     __syncthreads();
     const uint32_t bid = block_order(p.win);
@@ -249,6 +238,7 @@ __global__ __launch_bounds__(kWaveBlock) void gf8_mg_kernel(const Gf8MgParams<K>
     u32x4 d[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
+        MEC_DASSERT(!G || (p.src_off[j] >= 0 && p.src_off[j] < int64_t(p.sstride)));
         const uint64_t a = G ? uniform64(p.stab[gs * p.sstride + p.src_off[j]])
                              : uint64_t(uintptr_t(p.src + int64_t(stripe) * p.sss + p.src_off[j]));
         d[j] = buf_ld<u32x4>(chunk_rsrc(a, p.chunk), off, true);
@@ -258,6 +248,8 @@ __global__ __launch_bounds__(kWaveBlock) void gf8_mg_kernel(const Gf8MgParams<K>
         __amdgpu_buffer_rsrc_t dr[R];
 #pragma unroll
         for (int i = 0; i < R; ++i) {
+            MEC_DASSERT(g * R + i < uint32_t(kMaxSrc));
+            MEC_DASSERT(!G || p.dst_off[g * R + i] < int64_t(p.dstride));
             const int64_t o = p.dst_off[g * R + i];
             const uint64_t a = o < 0 ? 0 : G ? uniform64(p.dtab[gs * p.dstride + uint64_t(o)]) : uint64_t(uintptr_t(db + o));
             dr[i] = chunk_rsrc(a, p.chunk);
@@ -303,6 +295,16 @@ struct Gf8TailParams {
 
 hipError_t launch_gf8_tail(const Gf8Launch &L, uint64_t off, hipStream_t stream);
 
+// Launch one plan (launch_plan.cpp plan_gf8) with its kernel instantiation.
+template <int K, int R, bool G, int S>
+void launch_gf8_plan(const KernelPlan &pl, const Gf8Params<K, R> &p, hipStream_t stream) {
+    const dim3 grid(uint32_t(pl.grid)), block(pl.bt);
+    if (pl.bt == kWaveBlock)
+        hipLaunchKernelGGL((gf8_kernel<K, R, G, S, kWaveBlock>), grid, block, pl.lds_dynamic, stream, p);
+    else
+        hipLaunchKernelGGL((gf8_kernel<K, R, G, S, kThreads>), grid, block, pl.lds_dynamic, stream, p);
+}
+
 template <int K, int R>
 hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     Gf8Params<K, R> p;
@@ -313,82 +315,41 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
     p.sstride = L.sstride;
     p.dstride = L.dstride;
     p.chunk = uint32_t(L.len);
-    p.s0 = 0;
-    // block size from the whole launch's layout (sub-launches share it)
-    // one-wave blocks in place for stripe strides under kWaveBlockSpan,
-    // except strides of exactly 512 KiB and 1 MiB: there one-wave blocks
-    // decode at 62-71 % of 8 TB/s and 4-wave blocks at 77-82 %
-    // (tools/wpc_ab.py WPC_VAR=MEC_BLOCK, profiles/r02/wpc/win_pow2.log);
-    // other powers of two favour one-wave blocks like any stride (16 KiB:
-    // 69 -> 82 %, 2 MiB / 4 MiB +1-4; profiles/r02/gf8/rs_inplace_ab.log)
-    const int64_t sss = L.src_stripe_stride;
-    const bool wave_ok = sss >= 0 && sss < kWaveBlockSpan && sss != (int64_t(512) << 10) && sss != (int64_t(1) << 20);
-    const uint32_t bt = L.stab ? gathered_block_threads(L.gshape)
-                               : block_threads(true, launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
-                                                                    int64_t(L.n_stripes) * L.dst_stripe_stride),
-                                               wave_ok);
-    const Geometry g = geometry(L.len / 16, bt);
-    p.units = g.units;
-    p.tiles = g.tiles;
     p.accumulate = L.accumulate ? 1u : 0u;
-    p.win = 1;
-    p.nstr = 0;
-    p.sgroup = 0;
-    p.srun = 8;
     for (int j = 0; j < K; ++j) p.src_off[j] = L.src_off[j];
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int i = 0; i < R; ++i)
         for (int j = 0; j < K; ++j) p.coef[i][j] = L.coef[i][j];
-    const bool vand = gf8_structure(L.coef, K, R) == kGf8Vand;
-    if (g.units > 0) {
-        for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
-            const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-            if (L.stab) {
-                p.s0 = s0;
-                const dim3 grid(ns * g.tiles), block(bt);
-                const uint32_t lds = gathered_lds(bt, R * K * 32, L.gshape);
-                if (bt == kWaveBlock) {
-                    if (vand)
-                        hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Vand, kWaveBlock>), grid, block, lds, stream, p);
-                    else
-                        hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Dense, kWaveBlock>), grid, block, lds, stream, p);
-                } else {
-                    if (vand)
-                        hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Vand, kThreads>), grid, block, lds, stream, p);
-                    else
-                        hipLaunchKernelGGL((gf8_kernel<K, R, true, kGf8Dense, kThreads>), grid, block, lds, stream, p);
-                }
-            } else {
-                p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-                p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-                p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
-                p.nstr = ns;
-                p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
-                const bool in_place = p.win > 1;
-                const dim3 grid(ns * g.tiles), block(bt);
-                const uint32_t lds = occupancy_lds(bt, bt, R * K * 32, gf8_target_waves(K, R, in_place, !vand, L.accumulate));
-                if (L.probe) {
-                    if (bt == kWaveBlock)
-                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Xor, kWaveBlock>), grid, block, lds, stream, p);
-                    else
-                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Xor, kThreads>), grid, block, lds, stream, p);
-                } else if (bt == kWaveBlock) {
-                    if (vand)
-                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand, kWaveBlock>), grid, block, lds, stream, p);
-                    else
-                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Dense, kWaveBlock>), grid, block, lds, stream, p);
-                } else {
-                    if (vand)
-                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Vand, kThreads>), grid, block, lds, stream, p);
-                    else
-                        hipLaunchKernelGGL((gf8_kernel<K, R, false, kGf8Dense, kThreads>), grid, block, lds, stream, p);
-                }
-            }
-            hipError_t e = hipGetLastError();
-            if (e != hipSuccess) return e;
+    uint32_t units = 0;
+    for (uint32_t s0 = 0; s0 < L.n_stripes;) {
+        const KernelPlan pl = plan_gf8(L, s0);
+        if (!pl.ok || pl.k != K || pl.rows != R) return hipErrorInvalidValue;
+        units = pl.geo.units;
+        if (units == 0) break;
+        p.units = pl.geo.units;
+        p.tiles = pl.geo.tiles;
+        p.s0 = s0;
+        p.win = pl.win;
+        p.nstr = L.stab ? 0 : pl.ns;
+        p.sgroup = pl.sgroup;
+        p.srun = pl.srun;
+        p.src = L.stab ? nullptr : L.src + int64_t(s0) * L.src_stripe_stride;
+        p.dst = L.stab ? nullptr : L.dst + int64_t(s0) * L.dst_stripe_stride;
+        if (L.stab) {
+            if (pl.structure == kGf8Vand) launch_gf8_plan<K, R, true, kGf8Vand>(pl, p, stream);
+            else launch_gf8_plan<K, R, true, kGf8Dense>(pl, p, stream);
+        } else if (pl.structure == kGf8Xor) {
+            launch_gf8_plan<K, R, false, kGf8Xor>(pl, p, stream);
+        } else if (pl.structure == kGf8Vand) {
+            launch_gf8_plan<K, R, false, kGf8Vand>(pl, p, stream);
+        } else {
+            launch_gf8_plan<K, R, false, kGf8Dense>(pl, p, stream);
         }
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        s0 += pl.ns;
     }
-    if (L.len % 16) return launch_gf8_tail(L, uint64_t(g.units) * 16, stream);
+    if (L.len % 16) return launch_gf8_tail(L, uint64_t(L.len / 16) * 16, stream);
     return hipSuccess;
 }
 
@@ -402,44 +363,30 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
     p.dtab = L.dtab;
     p.sstride = L.sstride;
     p.dstride = L.dstride;
-    p.s0 = 0;
     p.chunk = uint32_t(L.len);
-    const Geometry g = geometry(L.len / 16, kWaveBlock);
-    p.units = g.units;
-    p.tiles = g.tiles;
     p.accumulate = L.accumulate ? 1u : 0u;
-    p.groups = uint32_t((L.rows + R - 1) / R);
     p.pad = 0;
     for (int j = 0; j < K; ++j) p.src_off[j] = L.src_off[j];
-    for (int r = 0; r < kMaxSrc; ++r) p.dst_off[r] = r < L.rows ? L.dst_off[r] : -1;
-    const uint32_t tab_bytes = p.groups * R * K * 32;
-    if (g.units == 0) return hipSuccess;
-    for (uint32_t s0 = 0; s0 < L.n_stripes; s0 += g.max_stripes_per_launch) {
-        const uint32_t ns = std::min(L.n_stripes - s0, g.max_stripes_per_launch);
-        if (L.stab) {  // pointer rows: no layout to window or group over
-            p.src = nullptr;
-            p.dst = nullptr;
-            p.s0 = s0;
-            p.win = 1;
-            p.nstr = 0;
-            p.sgroup = 0;
-            p.srun = 8;
-        } else {
-            p.src = L.src + int64_t(s0) * L.src_stripe_stride;
-            p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
-            p.win = launch_windows(p.src, int64_t(ns) * L.src_stripe_stride, p.dst, int64_t(ns) * L.dst_stripe_stride);
-            p.nstr = ns;
-            p.sgroup = stripe_group(L.len, g.tiles, p.win > 1 ? ns / p.win : ns, p.win > 1, false, p.srun);
-        }
-        // the tables are the block's LDS, and no wave cap: the caps of the
-        // <= 4-row launches (gf8_target_waves) starve these longer-computing
-        // waves — uncapped, RS(10,6)@256 KiB 67.2 -> 72.3 %, RS(8,5)@16 KiB
-        // 63.6 -> 66.5, ISA-L RS(12,8) 65.8 -> 67.2, the rest within 0.3
-        // (tools/wide_ab.py, profiles/r04/wide/mg_wpc_ab*.jsonl); MEC_WPC
-        // still forces one (experiments)
-        const uint32_t cap = occupancy_lds(kWaveBlock, kWaveBlock, 0, 0);
-        const uint32_t lds = std::max(cap, tab_bytes);
-        const dim3 grid(ns * g.tiles), block(kWaveBlock);
+    for (uint32_t s0 = 0; s0 < L.n_stripes;) {
+        const KernelPlan pl = plan_gf8_mg(L, s0);
+        // the plan bounds groups x R by the kernel's kMaxSrc output slots
+        if (!pl.ok || pl.k != K || pl.rows != R || pl.groups * uint32_t(R) > uint32_t(kMaxSrc))
+            return hipErrorInvalidValue;
+        if (pl.geo.units == 0) break;
+        p.groups = pl.groups;
+        for (int r = 0; r < kMaxSrc; ++r) p.dst_off[r] = r < L.rows ? L.dst_off[r] : -1;
+        p.units = pl.geo.units;
+        p.tiles = pl.geo.tiles;
+        p.s0 = s0;
+        p.win = pl.win;
+        p.nstr = L.stab ? 0 : pl.ns;
+        p.sgroup = pl.sgroup;
+        p.srun = pl.srun;
+        // pointer rows: no layout to window or group over
+        p.src = L.stab ? nullptr : L.src + int64_t(s0) * L.src_stripe_stride;
+        p.dst = L.stab ? nullptr : L.dst + int64_t(s0) * L.dst_stripe_stride;
+        const dim3 grid(uint32_t(pl.grid)), block(kWaveBlock);
+        const uint32_t lds = pl.lds_dynamic;
         if (L.stab) {
             if (L.vand)
                 hipLaunchKernelGGL((gf8_mg_kernel<K, R, kGf8Vand, true>), grid, block, lds, stream, p);
@@ -452,6 +399,7 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
         }
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+        s0 += pl.ns;
     }
     return hipSuccess;
 }

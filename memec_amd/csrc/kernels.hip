@@ -65,8 +65,10 @@ __global__ __launch_bounds__(kThreads) void gather_tail_kernel(const GatherParam
         const uint64_t a = srow[(D[sel_dw + j / 4] >> (8 * (j % 4))) & 0xffu];
         return a ? load_partial(reinterpret_cast<const uint8_t *>(a) + off + extra, n) : u32x4{0, 0, 0, 0};
     };
+    MEC_DASSERT(rows <= (bitmatrix ? uint32_t(kBmGatherRows) : uint32_t(kMaxRows)));
     for (uint32_t i = 0; i < rows; ++i) {
         const uint32_t sel = (D[dsel_dw + i / 4] >> (8 * (i % 4))) & 0xffu;
+        MEC_DASSERT(sel == kNoRow || sel < p.dstride);
         if (sel == kNoRow || !drow[sel]) continue;
         uint8_t *q0 = reinterpret_cast<uint8_t *>(drow[sel]) + off;
         if (!bitmatrix) {
@@ -224,157 +226,6 @@ hipError_t launch_bm_tail(const BmLaunch &L, uint64_t off, hipStream_t stream) {
 
 using namespace detail;
 
-namespace detail {
-uint32_t stripe_group(uint64_t chunk, uint32_t tiles, uint32_t n_stripes, bool in_place, bool bitmatrix,
-                      uint32_t &run) {
-    const int64_t kg = knob(kKnobSgroup), kr = knob(kKnobSrun);  // experiments (mec_set_knob)
-    run = 8;
-    // chunks of 2 MiB or more: 16 stripes, runs of 8 tiles
-    // (tools/sgroup_ab.py, profiles/r02/sgroup/; RS(10,4) split encode 2 MiB
-    // 75.7 -> 78.8-80.0 %, 4 MiB 72.4 -> 77.2, 8 MiB 67.1 -> 79.2, 16 MiB
-    // 57.4 -> 80.1; in-place decode 2 MiB 76.6 -> 78.5, 4 MiB 57.5 -> 76.0,
-    // 8 MiB 59.0 -> 78.1); at 256 KiB-1 MiB every group costs 1-10 points.
-    // Not for the bitmatrix kernel, whose lanes already read w packets a
-    // packet apart: CRS(12,4) 2 MiB encode 76.4 -> 72.8 %, decode 72.2 ->
-    // 68.7 with the same map (profiles/r02/sgroup/sgroup_ab_crs.log)
-    (void)in_place;
-    uint32_t g = (!bitmatrix && chunk >= (uint64_t(2) << 20)) ? 16u : 0u;
-    if (kg != kKnobUnset) {
-        g = uint32_t(std::max<int64_t>(kg, 0));
-        if (kr != kKnobUnset) run = uint32_t(std::max<int64_t>(kr, 0));
-    }
-    if (g <= 1 || run == 0 || run % 8 != 0 || tiles % run != 0 || n_stripes < 2) return 0;
-    return std::min(g, n_stripes);
-}
-
-uint32_t launch_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span) {
-    const int64_t forced = knob(kKnobWindows);  // experiments (mec_set_knob)
-    if (forced > 0) return uint32_t(forced);
-    const int64_t a0 = int64_t(reinterpret_cast<uintptr_t>(src)), b0 = int64_t(reinterpret_cast<uintptr_t>(dst));
-    const int64_t a1 = a0 + std::max<int64_t>(src_span, 0), b1 = b0 + std::max<int64_t>(dst_span, 0);
-    return (b0 < a1 && a0 < b1) ? 2u : 1u;
-}
-uint32_t bm_windows(const void *src, int64_t src_span, const void *dst, int64_t dst_span, uint64_t chunk, int rows,
-                    int k) {
-    const uint32_t w = launch_windows(src, src_span, dst, dst_span);
-    if (w <= 1 || knob(kKnobWindows) != kKnobUnset) return w;
-    // tiny in-place stripes take the split-layout launch: identity order,
-    // one-wave blocks, split caps (tools/bm_small_ab.py MEC_WINDOWS=1 arm,
-    // profiles/r03/bm_small_win1_ab_{1,2}.log, two rounds): 1 KiB chunks
-    // +2-16 points for every (k, m) tried, 2 KiB with <= 2 outputs and
-    // k >= 8 +0.6-2.5; 2 KiB with 4 outputs or k <= 6 and 4 KiB lose 0.5-4
-    const bool tiny = chunk <= 1024 || (chunk <= 2048 && rows <= 2 && k >= 8);
-    return tiny ? 1u : w;
-}
-uint32_t block_threads(bool strided, uint32_t win, bool wave_in_place) {
-    // gathered (pointer-table) launches are instantiated for kThreads only
-    if (!strided) return uint32_t(kThreads);
-    const int64_t forced = knob(kKnobBlock);  // experiments (mec_set_knob)
-    if (forced == kWaveBlock || forced == kThreads) return uint32_t(forced);
-    if (win == 1) return uint32_t(kWaveBlock);
-    return wave_in_place ? uint32_t(kWaveBlock) : uint32_t(kThreads);
-}
-uint32_t gathered_block_threads(uint8_t gshape) {
-    const int64_t e = knob(kKnobGblock);  // experiments (mec_set_knob)
-    if (e != kKnobUnset) return e == kWaveBlock ? uint32_t(kWaveBlock) : uint32_t(kThreads);
-    return gshape == 1 ? uint32_t(kWaveBlock) : uint32_t(kThreads);
-}
-namespace {
-// Dynamic LDS per block so that about `waves` active waves share a CU (each
-// block has `per` active waves); 0 when no LDS is left to reserve.
-uint32_t lds_for_waves(uint32_t per, uint32_t static_lds, uint32_t waves) {
-    constexpr uint32_t kLdsPerCu = 160u << 10, kGranule = 512;
-    const uint32_t blocks = std::max<uint32_t>(1, (waves + per - 1) / per);
-    const uint32_t per_block = kLdsPerCu / blocks / kGranule * kGranule;
-    const uint32_t used = (static_lds + kGranule - 1) / kGranule * kGranule;
-    return per_block > used + kGranule ? per_block - used - kGranule : 0;
-}
-}  // namespace
-
-uint32_t gathered_lds(uint32_t bt, uint32_t static_lds, uint8_t gshape) {
-    const int64_t e = knob(kKnobGwpc);  // experiments (mec_set_knob)
-    const int64_t w = e != kKnobUnset ? e : (gshape == 1 ? 16 : gshape == 2 ? 12 : 0);
-    if (w <= 0) return 0;
-    return lds_for_waves(std::max<uint32_t>(1, bt / 64), static_lds, uint32_t(w));
-}
-namespace {
-uint32_t ceil_even(double x) { return 2u * uint32_t(std::ceil(x / 2.0)); }
-uint32_t clampw(uint32_t w, uint32_t lo, uint32_t hi) { return std::min(hi, std::max(lo, w)); }
-}  // namespace
-
-uint32_t gf8_target_waves(int k, int rows, bool in_place, bool dense, bool accumulate) {
-    // read-modify-write of the outputs (delta updates, K = 1): each wave
-    // also loads its R outputs; R = 2 / 3 / 4 want 16-18 / 12 / 10-12
-    // waves (tools/bm_small_ab.py update, profiles/r02/gf8/update_caps.log:
-    // RS(10,4)@1 MiB update 81.7 -> 84.1 %)
-    if (accumulate && !in_place) return clampw(ceil_even(36.0 / std::max(1, rows)), 6, 20);
-    const double w = 64.0 / std::max(1, k) + (in_place ? 2.0 : 1.0) * rows;
-    // split layouts: a dense matrix (decode into separate output chunks,
-    // ISA-L Cauchy encode) computes ~30 % longer per wave than the
-    // Vandermonde encode, so it wants more waves to keep as many reads in
-    // flight: ceil_even(64/K + 2R), at most 16, never below the split
-    // count (tools/split_cap_ab.py, tools/split_rule_ab.py,
-    // profiles/r03/gf8/split_*.log: RS(10,4)@1 MiB decode_split 80.3 ->
-    // 83.5 %, (12,4)@64 KiB 75.4 -> 83.1, (16,4)@256 KiB 70.5 -> 80.0,
-    // (20,4)@16 KiB 68.9 -> 80.6; 20 waves cost (4,2)@4 KiB 1.1-1.8)
-    // Wide stripes with 4 output rows want more waves than 64/K + R gives,
-    // since a wave's K x R products keep it computing longer: at least
-    // ceil_even(K/2 + 1), at most 16 (tools/enc_cap_ab.py,
-    // profiles/r03/gf8/enc_cap_ab.log, enc_rule_ab*.log: RS and ISA-L RS
-    // (16,4)@256 KiB encode +1.0-1.9 points, (20,4)@16 KiB +4.0, (24,4)@64
-    // KiB +5.1-5.8, (28,4)@4 KiB +4.1; k <= 12 unchanged).  Two rows lose
-    // 1-3 points with the same floor ((18,2), (22,2), (30,2)), so they keep
-    // the plain count.
-    const uint32_t floor_wide = rows >= 4 ? std::min(ceil_even(0.5 * k + 1.0), 16u) : 0u;
-    const uint32_t split = clampw(std::max(ceil_even(w), floor_wide), 6, 20);
-    if (!in_place && dense)
-        return std::max(split, std::min(ceil_even(64.0 / std::max(1, k) + 2.0 * rows), 16u));
-    if (!in_place) return split;
-    // a dense (decode) matrix keeps each wave busy longer than the
-    // Vandermonde encode shortcut: at least 12 waves (RS(12,2) in-place
-    // decode at 128-256 KiB chunks 71 -> 76 %, RS(14,2) +1-2 points;
-    // profiles/r02/gf8/rs_inplace_ab.log, profiles/r02/wpc/wpc_pow2_strides.log)
-    if (dense) return clampw(std::max(ceil_even(w), 12u), 8, 24);
-    // the lighter Vandermonde encode in place wants the split count, 10..16
-    // (RS(10,4)@1 MiB 76.7 -> 79.5 %, RS(6,2)@256 KiB 81 -> 86 %;
-    // profiles/r02/gf8/rs104_valu_probe.log, rs_inplace_ab.log)
-    return clampw(ceil_even(64.0 / std::max(1, k) + rows), 10, 16);
-}
-
-uint32_t bm_lane_bytes(int w, int rows, uint64_t chunk, bool in_place) {
-    if (w > 4) return 8;
-    const int64_t e = knob(kKnobBmVw);  // experiments (mec_set_knob)
-    if (e != kKnobUnset) return e == 2 ? 8 : 16;
-    if (!in_place) return 8;
-    return (chunk <= (8u << 10) || (rows <= 2 && chunk <= (32u << 10))) ? 8 : 16;
-}
-
-uint32_t bm_target_waves(int rows, int w, int vw, bool in_place) {
-    // more than 4 outputs (wide codes): no cap — such a wave keeps rows x w
-    // packet slices and computes long enough that the caps below starve the
-    // stream (Cauchy(10,6)@64 KiB encode 74.6 -> 79.3 %, its in-place
-    // decode unchanged, Cauchy(8,5)@16 KiB +2.8, Cauchy(20,8) equal;
-    // tools/wide_ab.py, profiles/r04/wide/bm_wpc_ab*.jsonl)
-    if (rows > 4) return 0;
-    // w > 4 always runs 8-byte slices of twice as many packets: the
-    // 16-byte rule's bytes in flight per wave
-    if (vw >= 4 || w > 4) return clampw(uint32_t(3 * rows), 6, 16);
-    return in_place ? clampw(uint32_t(6 * rows), 6, 12) : clampw(uint32_t(6 * rows), 6, 16);
-}
-
-uint32_t occupancy_lds(uint32_t bt, uint32_t active, uint32_t static_lds, uint32_t waves) {
-    const int64_t e = knob(kKnobWpc);  // experiments (mec_set_knob)
-    const bool forced = e != kKnobUnset;
-    if (forced) waves = uint32_t(std::max<int64_t>(0, e));
-    // a block with less than one wave's worth of units streams too little
-    // per wave for a cap to pay (CRS at 2 KiB chunks: 75 % uncapped, 51 %
-    // capped, profiles/r02/sweep)
-    if (waves == 0 || (!forced && active < 64)) return 0;
-    const uint32_t act = std::min(bt, std::max<uint32_t>(active, 1));
-    return lds_for_waves(std::max<uint32_t>(1, (act + 63) / 64), static_lds, waves);
-}
-}  // namespace detail
-
 Gf8Coef gf8_coef(uint8_t c) {
     const Field &f = Field::get(8);
     auto pack = [&](unsigned a, unsigned b, unsigned cc, unsigned d) {
@@ -501,6 +352,9 @@ hipError_t launch_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
     if (L.k < 1 || L.k > kMaxK || L.rows <= kMaxRows || L.rows > kMaxSrc || !L.tabs || L.len % 16) return hipErrorInvalidValue;
     if (L.len == 0 || L.n_stripes == 0) return hipSuccess;
     if (L.len / 16 > uint64_t(UINT32_MAX)) return hipErrorInvalidValue;
+    // every group's rows index the kernel's kMaxSrc dst_off slots
+    if (L.group_rows < 1 || ((L.rows + L.group_rows - 1) / L.group_rows) * L.group_rows > kMaxSrc)
+        return hipErrorInvalidValue;
     if (L.group_rows == 8) {
         if (L.k < kMg8MinK || L.k > kMg8MaxK) return hipErrorInvalidValue;
         return kGfm8Table[size_t(L.k - kMg8MinK)](L, stream);
@@ -549,17 +403,13 @@ hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream) {
 
 hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, hipStream_t stream) {
     if (len == 0) return hipSuccess;
-    // one-wave blocks over 1 KiB tiles unless MEC_BLOCK=256, like the
-    // split-layout coding launches; 2 source streams + 1 output per lane:
-    // the gf8 split-layout cap
-    const uint32_t bt = block_threads(true, 1, false);
-    const uint64_t units = (len + 15) / 16, blocks = (units + bt - 1) / bt;
-    const uint32_t lds = occupancy_lds(bt, bt, 0, gf8_target_waves(2, 1, false, false, false));
-    const dim3 grid(uint32_t(std::min<uint64_t>(blocks, uint64_t(1) << 24)));
-    if (bt == kWaveBlock)
-        hipLaunchKernelGGL((xor_kernel<kWaveBlock>), grid, dim3(bt), lds, stream, dst, a, b, len);
+    const KernelPlan pl = plan_xor(len);
+    if (!pl.ok) return hipErrorInvalidValue;
+    const dim3 grid(uint32_t(pl.grid));
+    if (pl.bt == kWaveBlock)
+        hipLaunchKernelGGL((xor_kernel<kWaveBlock>), grid, dim3(pl.bt), pl.lds_dynamic, stream, dst, a, b, len);
     else
-        hipLaunchKernelGGL((xor_kernel<kThreads>), grid, dim3(bt), lds, stream, dst, a, b, len);
+        hipLaunchKernelGGL((xor_kernel<kThreads>), grid, dim3(pl.bt), pl.lds_dynamic, stream, dst, a, b, len);
     return hipGetLastError();
 }
 

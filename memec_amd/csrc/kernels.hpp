@@ -61,7 +61,7 @@ struct BmLaunch {
     uint32_t sstride, dstride;
     int64_t src_off[kMaxSrc];
     int64_t dst_off[kMaxBmOut];
-    int k, rows, w;        // rows = output chunks (each w packets), <= kMaxRows when gathered
+    int k, rows, w;        // rows = output chunks (each w packets), <= kMaxBmOut = 8 (strided and gathered)
     uint64_t packet;
     uint32_t n_stripes;
     bool accumulate;

@@ -1,8 +1,10 @@
 // knobs.cpp — experiment overrides, read from the environment once (see
-// knobs.hpp).
+// knobs.hpp), every value validated against its knob's accepted set.
 #include "knobs.hpp"
 
 #include <atomic>
+#include <cerrno>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -10,47 +12,79 @@ namespace mec {
 namespace detail {
 namespace {
 
-// every knob's variable (the environment is read for each, once)
-constexpr const char *kEnvNames[] = {"MEC_SGROUP", "MEC_WINDOWS",      "MEC_BLOCK", "MEC_GBLOCK",  "MEC_GWPC",
-                                     "MEC_BM_VW",  "MEC_WPC",          "MEC_COPY_THREADS", "MEC_WIDE",
-                                     "MEC_MG_ROWS"};
-// MEC_SGROUP sets two knobs (group and run), every other name one
-static_assert(sizeof(kEnvNames) / sizeof(kEnvNames[0]) == kKnobCount - 1, "a knob whose variable is never read");
+// Accepted values.  Wave caps: 0 (no cap) .. 32 waves per CU (the gfx950
+// limit); windows 1..16; MEC_SGROUP groups 0..64 stripes (0 / 1 = identity
+// map) with runs of 8..1024 tiles in steps of 8 (stripe_tile's contract).
+constexpr KnobSpec kSpecs[] = {
+    {"MEC_SGROUP", kKnobSgroup, 0, 64, {}, 0},
+    {"MEC_WINDOWS", kKnobWindows, 1, 16, {}, 0},
+    {"MEC_BLOCK", kKnobBlock, 64, 256, {64, 256}, 2},
+    {"MEC_GBLOCK", kKnobGblock, 64, 256, {64, 256}, 2},
+    {"MEC_GWPC", kKnobGwpc, 0, 32, {}, 0},
+    {"MEC_BM_VW", kKnobBmVw, 2, 4, {2, 4}, 2},
+    {"MEC_WPC", kKnobWpc, 0, 32, {}, 0},
+    {"MEC_COPY_THREADS", kKnobCopyThreads, 1, 64, {}, 0},
+    {"MEC_WIDE", kKnobWide, 0, 1, {}, 0},
+    {"MEC_MG_ROWS", kKnobMgRows, 3, 8, {3, 4, 8}, 3},
+};
+// every knob but MEC_SGROUP's run half has its own variable
+static_assert(sizeof(kSpecs) / sizeof(kSpecs[0]) == kKnobCount - 1, "a knob whose variable is never read");
+
+// A whole decimal integer (optionally signed), nothing else.
+bool parse_int(const char *s, const char *end, int64_t &out) {
+    if (s == end) return false;
+    char buf[32];
+    const size_t n = size_t(end - s);
+    if (n >= sizeof buf) return false;
+    std::memcpy(buf, s, n);
+    buf[n] = 0;
+    char *e = nullptr;
+    errno = 0;
+    const long long v = std::strtoll(buf, &e, 10);
+    if (errno || e != buf + n) return false;
+    out = int64_t(v);
+    return true;
+}
+
+bool accepted(const KnobSpec &s, int64_t v) {
+    if (v < s.lo || v > s.hi) return false;
+    if (s.nset == 0) return true;
+    for (int i = 0; i < s.nset; ++i)
+        if (s.set[i] == v) return true;
+    return false;
+}
 
 struct Knobs {
     std::atomic<int64_t> v[kKnobCount];
     Knobs() {
         for (auto &x : v) x.store(kKnobUnset, std::memory_order_relaxed);
-        for (const char *n : kEnvNames) apply(n, std::getenv(n));
-    }
-    bool apply(const char *name, const char *value) {
-        auto put = [&](Knob k, int64_t x) { v[k].store(x, std::memory_order_relaxed); };
-        const bool unset = value == nullptr;
-        const int64_t num = unset ? kKnobUnset : int64_t(std::atoll(value));
-        if (!std::strcmp(name, "MEC_SGROUP")) {
-            if (unset) {
-                put(kKnobSgroup, kKnobUnset);
-                put(kKnobSrun, kKnobUnset);
-            } else {
-                put(kKnobSgroup, num);
-                const char *c = std::strchr(value, ':');
-                put(kKnobSrun, c ? int64_t(std::atoll(c + 1)) : kKnobUnset);
-            }
-            return true;
+        for (const KnobSpec &s : kSpecs) {
+            const char *e = std::getenv(s.name);
+            if (e && apply(s, e) != KnobStatus::kOk)
+                std::fprintf(stderr, "libmec: %s=%s is not an accepted value; the built-in rule applies\n", s.name, e);
         }
-        static const struct {
-            const char *name;
-            Knob k;
-        } kPlain[] = {{"MEC_WINDOWS", kKnobWindows}, {"MEC_BLOCK", kKnobBlock},   {"MEC_GBLOCK", kKnobGblock},
-                      {"MEC_GWPC", kKnobGwpc},       {"MEC_BM_VW", kKnobBmVw},     {"MEC_WPC", kKnobWpc},
-                      {"MEC_COPY_THREADS", kKnobCopyThreads}, {"MEC_WIDE", kKnobWide},
-                      {"MEC_MG_ROWS", kKnobMgRows}};
-        for (const auto &p : kPlain)
-            if (!std::strcmp(name, p.name)) {
-                put(p.k, num);
-                return true;
-            }
-        return false;
+    }
+    KnobStatus apply(const KnobSpec &s, const char *value) {
+        auto put = [&](Knob k, int64_t x) { v[k].store(x, std::memory_order_relaxed); };
+        if (!value) {
+            put(s.knob, kKnobUnset);
+            if (s.knob == kKnobSgroup) put(kKnobSrun, kKnobUnset);
+            return KnobStatus::kOk;
+        }
+        const char *end = value + std::strlen(value);
+        if (s.knob == kKnobSgroup) {
+            const char *c = std::strchr(value, ':');
+            int64_t g = 0, r = kKnobUnset;
+            if (!parse_int(value, c ? c : end, g) || !accepted(s, g)) return KnobStatus::kInvalid;
+            if (c && (!parse_int(c + 1, end, r) || r < 8 || r > kSrunMax || r % 8 != 0)) return KnobStatus::kInvalid;
+            put(kKnobSgroup, g);
+            put(kKnobSrun, r);
+            return KnobStatus::kOk;
+        }
+        int64_t x = 0;
+        if (!parse_int(value, end, x) || !accepted(s, x)) return KnobStatus::kInvalid;
+        put(s.knob, x);
+        return KnobStatus::kOk;
     }
 };
 
@@ -61,9 +95,19 @@ Knobs &knobs() {
 
 }  // namespace
 
+const KnobSpec *knob_specs(int &n) {
+    n = int(sizeof(kSpecs) / sizeof(kSpecs[0]));
+    return kSpecs;
+}
+
 int64_t knob(Knob k) { return knobs().v[k].load(std::memory_order_relaxed); }
 
-bool set_knob(const char *name, const char *value) { return name && knobs().apply(name, value); }
+KnobStatus set_knob(const char *name, const char *value) {
+    if (!name) return KnobStatus::kUnknown;
+    for (const KnobSpec &s : kSpecs)
+        if (!std::strcmp(name, s.name)) return knobs().apply(s, value);
+    return KnobStatus::kUnknown;
+}
 
 }  // namespace detail
 }  // namespace mec

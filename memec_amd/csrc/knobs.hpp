@@ -5,6 +5,14 @@
 // run time.  No launch path calls getenv, so the library never races a
 // caller's setenv/putenv, and an experiment flips a knob between launches
 // through the API instead of the environment.
+//
+// Every value is validated where it enters (knob_spec): a value outside a
+// knob's accepted set is refused by mec_set_knob (MEC_EINVAL) and ignored,
+// with a warning, when it comes from the environment, so a launch never sees
+// it.  Combinations that depend on the launch (MEC_MG_ROWS against the row
+// count, wave caps against the LDS a block already uses) are resolved by the
+// launch planner (launch_plan.cpp), which falls back to the built-in rule
+// rather than issue a launch outside its invariants.
 #pragma once
 
 #include <cstdint>
@@ -28,11 +36,26 @@ enum Knob : int {
 };
 constexpr int64_t kKnobUnset = INT64_MIN;
 
+// Accepted values of one knob: lo..hi, and when `set` is non-empty only the
+// values it lists (terminated by 0 unless 0 itself is listed first).
+struct KnobSpec {
+    const char *name;  // environment variable
+    Knob knob;
+    int64_t lo, hi;
+    int64_t set[4];
+    int nset;
+};
+// The table (knobs.cpp); MEC_SGROUP's run half is checked with it.
+const KnobSpec *knob_specs(int &n);
+// Accepted range of MEC_SGROUP's run (a multiple of 8).
+constexpr int64_t kSrunMax = 1024;
+
 // Current value, or kKnobUnset.
 int64_t knob(Knob k);
 // name: the environment variable's name ("MEC_WPC", ...); value: the same
-// syntax as the variable, NULL = unset.  Returns false for an unknown name.
-bool set_knob(const char *name, const char *value);
+// syntax as the variable, NULL = unset.
+enum class KnobStatus { kOk, kUnknown, kInvalid };
+KnobStatus set_knob(const char *name, const char *value);
 
 }  // namespace detail
 }  // namespace mec

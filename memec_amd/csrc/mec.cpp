@@ -4,6 +4,7 @@
 // coalescer live in batch.cpp.
 #include "ctx.hpp"
 #include "knobs.hpp"
+#include "launch_plan.hpp"
 
 #include <chrono>
 #include <cstdarg>
@@ -45,44 +46,89 @@ void bit_block(const Field &f, unsigned e, uint32_t w, uint8_t *mask, size_t mst
     }
 }
 
-// The device copy of coef's multi-group permute tables (gf8_mg_kernel),
-// uploaded at first use and kept for the context's lifetime.
-int mg_tables(mec_ctx *c, const Mat &coef, size_t rows, size_t ns, int R, const uint32_t *&out) {
+// The device copy of coef's multi-group permute tables (gf8_mg_kernel):
+// looked up, or built into the arena's pinned mirror and uploaded with an
+// async copy on `stream` (no blocking hipMalloc / hipMemcpy on the null
+// stream inside a stream-ordered call; an arena block is allocated once per
+// 4 MiB of tables).  kMgUncached past the cache's cap.
+int mg_tables(mec_ctx *c, const Mat &coef, size_t rows, size_t ns, int R, hipStream_t stream, const uint32_t *&out) {
     std::string key(reinterpret_cast<const char *>(coef.data()), rows * ns);
     key += char(rows);
     key += char(ns);
     key += char(R);
-    std::lock_guard<std::mutex> g(c->mg_mu);
-    auto it = c->mg_tabs.find(key);
-    if (it != c->mg_tabs.end()) {
-        out = it->second;
+    MgCache &M = c->mg;
+    std::lock_guard<std::mutex> g(M.mu);
+    auto it = M.map.find(key);
+    if (it != M.map.end()) {
+        MgEntry &e = it->second;
+        if (!e.landed) {
+            const hipError_t q = hipEventQuery(e.ready);
+            if (q == hipSuccess) e.landed = true;
+            else if (q == hipErrorNotReady) HIP_TRY(hipStreamWaitEvent(stream, e.ready, 0));
+            else return hip_fail(q, "mg tables upload");
+        }
+        out = e.dev;
         return MEC_OK;
     }
     std::vector<uint32_t> img;
     mec::gf8_mg_tables(coef.data(), int(rows), int(ns), R, img);
-    uint32_t *d = nullptr;
-    DeviceGuard dg(c->device);
-    HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), img.size() * sizeof(uint32_t)));
-    const hipError_t e = hipMemcpy(d, img.data(), img.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        (void)hipFree(d);
-        return hip_fail(e, "mg tables");
+    const size_t bytes = (img.size() * sizeof(uint32_t) + 255) & ~size_t(255);
+    if (M.bytes + bytes > M.cap || bytes > kMgBlock) {
+        M.uncached++;
+        return kMgUncached;
     }
-    c->mg_tabs.emplace(key, d);
-    out = d;
+    DeviceGuard dg(c->device);
+    if (M.dev_blocks.empty() || M.block_used + bytes > kMgBlock) {
+        uint8_t *d = nullptr, *h = nullptr;
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&d), kMgBlock));
+        const hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&h), kMgBlock, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            (void)hipFree(d);
+            return hip_fail(e, "mg tables staging");
+        }
+        M.dev_blocks.push_back(d);
+        M.host_blocks.push_back(h);
+        M.block_used = 0;
+    }
+    uint8_t *hd = M.host_blocks.back() + M.block_used, *dd = M.dev_blocks.back() + M.block_used;
+    std::memcpy(hd, img.data(), img.size() * sizeof(uint32_t));
+    MgEntry e;
+    HIP_TRY(hipEventCreateWithFlags(&e.ready, hipEventDisableTiming));
+    hipError_t err = hipMemcpyAsync(dd, hd, img.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream);
+    if (err == hipSuccess) err = hipEventRecord(e.ready, stream);
+    if (err != hipSuccess) {
+        (void)hipEventDestroy(e.ready);
+        return hip_fail(err, "mg tables upload");
+    }
+    e.dev = reinterpret_cast<const uint32_t *>(dd);
+    M.block_used += bytes;
+    M.bytes += bytes;
+    M.map.emplace(key, e);
+    out = e.dev;
     return MEC_OK;
 }
 
-int mg_prepare(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, Gf8MgLaunch &L) {
+void mg_release(mec_ctx *c) {
+    MgCache &M = c->mg;
+    for (auto &kv : M.map)
+        if (kv.second.ready) {
+            (void)hipEventSynchronize(kv.second.ready);
+            (void)hipEventDestroy(kv.second.ready);
+        }
+    M.map.clear();
+    for (uint8_t *d : M.dev_blocks) (void)hipFree(d);
+    for (uint8_t *h : M.host_blocks) (void)hipHostFree(h);
+    M.dev_blocks.clear();
+    M.host_blocks.clear();
+}
+
+int mg_prepare(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, Gf8MgLaunch &L, hipStream_t stream) {
     bool vand = true;  // row 0 and column 0 all ones (Jerasure / ISA-L RS parity rows)
     for (size_t j = 0; j < ns && vand; ++j) vand = coef[j] == 1;
     for (size_t r = 0; r < nd && vand; ++r) vand = coef[r * ns] == 1;
     L.vand = vand;
-    L.group_rows = mec::gf8_mg_rows(int(nd), int(ns), vand);
-    const int64_t kr = mec::detail::knob(mec::detail::kKnobMgRows);  // experiments (mec_set_knob)
-    if (kr == 3 || kr == 4 || (kr == 8 && ns >= size_t(mec::kMg8MinK) && ns <= size_t(mec::kMg8MaxK)))
-        L.group_rows = int(kr);
-    return mg_tables(c, coef, nd, ns, L.group_rows, L.tabs);
+    L.group_rows = mec::detail::mg_group_rows(int(nd), int(ns), vand);
+    return mg_tables(c, coef, nd, ns, L.group_rows, stream, L.tabs);
 }
 
 bool mg_wanted(const mec_ctx *c, size_t nd) {
@@ -116,10 +162,13 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
         L.accumulate = accumulate;
         for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
         for (size_t r = 0; r < nd; ++r) L.dst_off[r] = lay.dst_off[r];
-        int rc = mg_prepare(c, coef, nd, ns, L);
-        if (rc != MEC_OK) return rc;
-        HIP_TRY(mec::launch_gf8_mg(L, stream));
-        return MEC_OK;
+        const int rc = mg_prepare(c, coef, nd, ns, L, stream);
+        if (rc == MEC_OK) {
+            HIP_TRY(mec::launch_gf8_mg(L, stream));
+            return MEC_OK;
+        }
+        if (rc != kMgUncached) return rc;
+        // past the table cache's cap: groups of 4 rows below
     }
     const size_t step = c->byte_wise() ? size_t(mec::kMaxRows) : size_t(mec::kMaxBmOut);
     for (size_t r0 = 0; r0 < nd; r0 += step) {
@@ -377,6 +426,10 @@ int mec_create(int family, uint32_t k, uint32_t m, uint32_t chunk_size, int devi
             break;
     }
     c->packet = family == MEC_CAUCHY_GOOD ? chunk_size / c->w : chunk_size;
+    {  // one-pass table cache cap (read here, never on a launch path)
+        const char *e = std::getenv("MEC_MG_CACHE_BYTES");
+        c->mg.cap = e && *e ? size_t(std::strtoull(e, nullptr, 10)) : (size_t(64) << 20);
+    }
     if (device >= 0) {
         int n = 0;
         hipError_t e = hipGetDeviceCount(&n);
@@ -399,9 +452,13 @@ void mec_destroy(mec_ctx *c) {
     c->shards.clear();
     if (has_device(c)) {
         DeviceGuard g(c->device);
-        queue_stop(c);  // the resident kernel returns before anything is freed
+        // the resident kernel returns before anything is freed; a grid still
+        // running at the drain cap (a hung job) may yet read a staging lane's
+        // sources and write its outputs, so the lanes are leaked with it
+        const bool drained = queue_stop(c);
         batch_release(c);
         for (Lane *l : c->lanes_all) {
+            if (!drained) break;
             (void)hipStreamSynchronize(l->stream);
             (void)hipHostFree(l->host);
             (void)hipStreamDestroy(l->stream);
@@ -414,7 +471,7 @@ void mec_destroy(mec_ctx *c) {
             }
             if (c->bdev[i]) (void)hipFree(c->bdev[i]);
         }
-        for (auto &t : c->mg_tabs) (void)hipFree(t.second);
+        mg_release(c);
     }
     delete c;
 }
@@ -522,8 +579,11 @@ int mec_set_probe(mec_ctx *c, int mode) {
 
 int mec_set_knob(const char *name, const char *value) {
     if (!name) return fail(MEC_EINVAL, "null knob name");
-    if (!mec::detail::set_knob(name, value)) return fail(MEC_EINVAL, "unknown knob %s", name);
-    return MEC_OK;
+    switch (mec::detail::set_knob(name, value)) {
+        case mec::detail::KnobStatus::kOk: return MEC_OK;
+        case mec::detail::KnobStatus::kUnknown: return fail(MEC_EINVAL, "unknown knob %s", name);
+        default: return fail(MEC_EINVAL, "%s=%s is not an accepted value", name, value ? value : "(null)");
+    }
 }
 
 int mec_fill_random(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_offset, void *stream) {

@@ -363,6 +363,7 @@ __global__ __launch_bounds__(kQThreads) void queue_kernel(QSlot *slots, const ui
         }
         __syncthreads();
         const uint32_t ns = hdr[0], nd = hdr[1], bytes = hdr[2], acc_in = hdr[3], w = hdr[4], P = hdr[5];
+        MEC_DASSERT(ns <= kQMaxSrc && nd <= kQMaxDst && ns == (shape >> 8) && nd == (shape & 0xffu) && w <= 8);
         const bool traced = hdr[6] != 0u && part == 0 && t == 0;
         const uint64_t t_desc = traced ? __builtin_amdgcn_s_memrealtime() : 0;
         if (w == 0) {  // byte-wise GF(2^8): the host's v_perm tables, read in place from LDS
@@ -487,9 +488,9 @@ Drain queue_drained(HostQueue *q, int ms) {
 
 }  // namespace
 
-void queue_stop(mec_ctx *c) {
+bool queue_stop(mec_ctx *c) {
     HostQueue *q = c->hq;
-    if (!q) return;
+    if (!q) return true;
     c->hq = nullptr;
     {
         DeviceGuard dg(c->device);
@@ -499,7 +500,7 @@ void queue_stop(mec_ctx *c) {
         // slots and control words under a running kernel would fault it
         if (queue_drained(q, int(std::max<uint64_t>(q->timeout_ms, 1000))) == Drain::kRunning) {
             fprintf(stderr, "libmec: host queue kernel still running at mec_destroy; its memory is leaked\n");
-            return;
+            return false;
         }
         (void)hipStreamDestroy(q->stream);
         (void)hipHostFree(q->host);
@@ -510,6 +511,7 @@ void queue_stop(mec_ctx *c) {
     delete[] q->busy;
     delete[] q->seqno;
     delete q;
+    return true;
 }
 
 int queue_start(mec_ctx *c, uint32_t slots) {
@@ -814,7 +816,7 @@ int mec_set_host_queue(mec_ctx *c, uint32_t slots) {
     }
     if (!c->shards.empty()) return MEC_OK;  // a multi-device context's host calls all go to its shards
     std::lock_guard<std::mutex> g(c->hq_mu);
-    queue_stop(c);
+    if (!queue_stop(c)) return fail(MEC_EHIP, "the host queue kernel did not leave; its memory is leaked");
     return slots ? queue_start(c, slots) : MEC_OK;
 }
 

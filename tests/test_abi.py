@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(_lib.SYMBOLS)
-    assert L.mec_abi_version() == 4
+    assert L.mec_abi_version() == 5
 
 
 def test_coding_adapter_library_links():
@@ -163,20 +163,29 @@ def test_knobs_through_the_api_not_the_environment():
         memec_amd.set_knob(name, None)
     with pytest.raises(MecError):
         memec_amd.set_knob("MEC_NO_SUCH_KNOB", "1")
+    # values outside a knob's accepted set are refused (knobs.cpp kSpecs)
+    for name, value in (("MEC_MG_ROWS", "5"), ("MEC_BLOCK", "128"), ("MEC_WPC", "33"), ("MEC_WPC", "1x"),
+                        ("MEC_WINDOWS", "0"), ("MEC_SGROUP", "4:7"), ("MEC_BM_VW", "3"), ("MEC_WIDE", "2")):
+        with pytest.raises(MecError) as e:
+            memec_amd.set_knob(name, value)
+        assert "accepted" in str(e.value), (name, value)
     src = open(os.path.join(ROOT, "memec_amd", "csrc", "kernels.hip")).read()
     assert "getenv" not in src
 
 
 def test_every_knob_is_read_from_the_environment():
-    """knobs.cpp reads each knob's variable once at first use; a knob that
-    mec_set_knob accepts but the environment list misses is silently
-    ignored when set by variable (round 4: MEC_MG_ROWS and a since-removed knob were,
-    which voided an A/B run through the environment)."""
+    """knobs.cpp reads each knob's variable once at first use, from one
+    table (kSpecs) that also holds its accepted values; every knob of the
+    Knob enum has an entry (a static assert) and mec.h documents each
+    variable (round 4: MEC_MG_ROWS was accepted by mec_set_knob but never
+    read from the environment, which voided an A/B run)."""
     import re
     src = open(os.path.join(ROOT, "memec_amd", "csrc", "knobs.cpp")).read()
-    env = set(re.findall(r'"(MEC_[A-Z_]+)"', src[src.index("kEnvNames[]"):src.index("};", src.index("kEnvNames[]"))]))
-    plain = set(re.findall(r'\{"(MEC_[A-Z_]+)", kKnob', src))
-    assert plain | {"MEC_SGROUP"} == env
+    table = src[src.index("kSpecs[] = {"):src.index("};", src.index("kSpecs[] = {"))]
+    env = set(re.findall(r'\{"(MEC_[A-Z_]+)", kKnob', table))
+    hdr_k = open(os.path.join(ROOT, "memec_amd", "csrc", "knobs.hpp")).read()
+    knobs_enum = set(re.findall(r"// (MEC_[A-Z_]+)=", hdr_k))
+    assert env == knobs_enum, (env ^ knobs_enum)
     hdr = open(os.path.join(ROOT, "include", "mec.h")).read()
     for name in env:
         assert name in hdr, name
@@ -185,3 +194,30 @@ def test_every_knob_is_read_from_the_environment():
 def test_probe_needs_a_context():
     L = _lib.lib()
     assert L.mec_set_probe(None, 1) == _lib.MEC_EINVAL
+
+
+def test_launch_planner_invariants_every_knob(tmp_path):
+    """tests/cpp/launch_plan_check.cc: the launch planner
+    (memec_amd/csrc/launch_plan.cpp, the only source of every launch's
+    shape) under every accepted value of every MEC_* knob, ~10^8 plans of
+    gf8 / one-pass / bitmatrix / gathered / XOR launches: rows per group x
+    groups <= 32 (the round-4 MEC_MG_ROWS=3 overrun,
+    profiles/r05/parity/launch_plan_check_before_fix.log), LDS <= 160 KiB,
+    instantiated templates and block sizes only, 32-bit lane offsets,
+    stripe-group runs that tile the stripe, sub-launches covering the batch,
+    and no legal call refused.  Host code only (g++, UBSan)."""
+    import shutil
+    import subprocess
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "launch_plan_check")
+    csrc = os.path.join(ROOT, "memec_amd", "csrc")
+    subprocess.check_call(["g++", "-std=c++17", "-O2", "-fsanitize=undefined", "-fno-sanitize-recover=undefined",
+                           "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", "-I" + os.path.join(ROOT, "include"),
+                           "-I" + csrc, os.path.join(ROOT, "tests", "cpp", "launch_plan_check.cc"),
+                           os.path.join(csrc, "launch_plan.cpp"), os.path.join(csrc, "knobs.cpp"), "-o", exe])
+    env = {k: v for k, v in os.environ.items() if not k.startswith("MEC_")}
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-2000:]
+    assert out.stdout.startswith("ok "), out.stdout
+    assert int(out.stdout.split()[1]) > 10 ** 8

@@ -17,7 +17,7 @@ import _oracle as O
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-from memec_amd import Codec  # noqa: E402
+from memec_amd import Codec, MecError  # noqa: E402
 
 K, M, N = 6, 3, 20
 ERASED = (0, 4, 7)
@@ -138,12 +138,17 @@ def _stripes_km(fam, k, m, cs, n, seed):
     return base
 
 
-@pytest.mark.parametrize("group", ["0", "3:8", "7:16", "4:64", "64:8", "bad:7"])
+@pytest.mark.parametrize("group", ["0", "3:8", "7:16", "4:64", "64:8", "5:128"])
 def test_stripe_group_overrides(group, knobs):
     """The stripe-group block map (stream_common.hpp stripe_tile) with
     forced groups and run lengths, a last group shorter than the rest
-    (N = 20 stripes), and an invalid run (falls back to the identity map):
-    every layout stays bit-exact.  64 KiB chunks: 64 one-wave tiles."""
+    (N = 20 stripes), and a run that does not tile the stripe (128 of 64
+    tiles: the planner keeps the identity map); every layout stays
+    bit-exact.  64 KiB chunks: 64 one-wave tiles.  Values outside the
+    accepted set (a run of 7, a non-number) are refused at mec_set_knob."""
+    for bad in ("bad:7", "4:7", "65"):
+        with pytest.raises(MecError):
+            knobs("MEC_SGROUP", bad)
     knobs("MEC_SGROUP", group)
     _check_all_layouts("rs", 65536, 1500)
 

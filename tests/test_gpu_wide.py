@@ -152,6 +152,81 @@ def test_wide_group_rows_forced(fam, rows, knobs):
         c.close()
 
 
+@pytest.mark.parametrize("fam", ["rs", "isal_rs"])
+def test_forced_three_row_groups_31_rows(fam, knobs):
+    """RS(1,31) with MEC_MG_ROWS=3: 31 rows in groups
+    of 3 would be 11 groups, 33 of the one-pass kernel's 32 output slots —
+    the round-4 library read dst_off[32] past its kernel arguments.  The
+    planner now keeps the forced count only where the groups fit and falls
+    back to the rule (8 groups of 4) here; encode, a 30-erasure in-place
+    decode and an accumulating update equal the oracle, and RS(1,30) keeps
+    the forced 10 x 3 groups."""
+    knobs("MEC_MG_ROWS", "3")
+    for k, m in [(1, 31), (1, 30), (2, 30)]:
+        cs, n = 512, 3
+        data = O.fill(n * k * cs, 900 + m).reshape(n, k, cs)
+        want = np.stack([np.stack(O.encode(fam, k, m, [data[s, j].copy() for j in range(k)], cs)) for s in range(n)])
+        c = Codec(fam, k, m, cs)
+        st = torch.zeros(n, k + m, cs, dtype=torch.uint8, device=DEV)
+        st[:, :k] = dev(data)
+        c.encode(st[:, :k], st[:, k:])
+        assert np.array_equal(host(st[:, k:]), want), (fam, k, m)
+        keep = k + m - 1  # only the last parity survives (k = 1) / two chunks (k = 2)
+        pat = [i for i in range(k + m) if i != keep and (k == 1 or i != 0)]
+        t = st.clone()
+        t[:, pat] = 0
+        c.decode(t, sum(1 << i for i in range(k + m) if i not in pat))
+        torch.cuda.synchronize()
+        assert torch.equal(t, st), (fam, k, m)
+        delta = O.fill(n * cs, 901 + m).reshape(n, cs)
+        d2 = data.copy()
+        d2[:, 0] ^= delta
+        par = st[:, k:].clone()
+        c.encode_update(0, dev(delta), par)
+        want2 = np.stack([np.stack(O.encode(fam, k, m, [d2[s, j].copy() for j in range(k)], cs)) for s in range(n)])
+        assert np.array_equal(host(par), want2), (fam, k, m, "update")
+        c.close()
+
+
+def test_one_pass_table_cache_is_bounded(monkeypatch):
+    """The one-pass kernel's permute tables are cached per matrix up to
+    MEC_MG_CACHE_BYTES (the cache grew without bound, one
+    device allocation per erasure pattern).  RS(16,8) decodes of 60
+    distinct 5..8-erasure patterns under a 3-table cap: every stripe is
+    rebuilt, the cache holds at most the cap, the patterns past it ran as
+    4-row launches, and no device memory leaks past the cap."""
+    k, m, cs, n = 16, 8, 1024, 2
+    monkeypatch.setenv("MEC_MG_CACHE_BYTES", str(3 * 8 * 16 * 32))
+    c = Codec("rs", k, m, cs)
+    data = O.fill(n * k * cs, 321).reshape(n, k, cs)
+    st = torch.zeros(n, k + m, cs, dtype=torch.uint8, device=DEV)
+    st[:, :k] = dev(data)
+    c.encode(st[:, :k], st[:, k:])
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    rng = np.random.default_rng(5)
+    seen = set()
+    while len(seen) < 60:
+        e = int(rng.integers(5, m + 1))
+        pat = tuple(sorted(rng.choice(k + m, size=e, replace=False).tolist()))
+        if pat in seen:
+            continue
+        seen.add(pat)
+        t = st.clone()
+        t[:, list(pat)] = 0
+        c.decode(t, sum(1 << i for i in range(k + m) if i not in pat))
+        torch.cuda.synchronize()
+        assert torch.equal(t, st), pat
+        del t
+    s = c.stats()
+    assert s["mg_cache_bytes"] <= 3 * 8 * 16 * 32, s
+    assert 1 <= s["mg_cache_tables"] <= 4, s
+    assert s["mg_cache_uncached"] >= 50, s
+    # one 4 MiB arena block at most (plus torch's own caching slack)
+    assert free0 - torch.cuda.mem_get_info()[0] <= (8 << 20), (free0, torch.cuda.mem_get_info()[0])
+    c.close()
+
+
 @pytest.mark.parametrize("fam", ["rs", "cauchy", "isal_rs"])
 def test_wide_roundtrip_every_pattern_small(fam):
     """RS(3,6)-sized code: every erasure pattern of 5 and 6 chunks."""
@@ -197,12 +272,15 @@ def test_wide_update_linearity(fam):
 from test_gpu_batch import Slab, chunk_of, random_patterns, zeros  # noqa: E402
 
 
+@pytest.mark.parametrize("cs", [1024, 1032])
 @pytest.mark.parametrize("mem", ["device", "host"])
 @pytest.mark.parametrize("fam", FAMS)
-def test_wide_encode_batch_scattered(fam, mem):
+def test_wide_encode_batch_scattered(fam, mem, cs):
     """mec_encode_batch with 7 parities (row groups of 4 + 3), scattered
-    ChunkPool-like slots, Coding::zeros columns and unwanted parities."""
-    k, m, cs, n = 10, 7, 1024, 24
+    ChunkPool-like slots, Coding::zeros columns and unwanted parities;
+    cs = 1032 has an 8-byte tail (the per-row-group tail
+    launches of multi-map wide batches were untested)."""
+    k, m, n = 10, 7, 24
     if fam == "cauchy" and not ok_shape(fam, k, m, cs):
         pytest.skip("no Cauchy w")
     rng = np.random.default_rng(17)
@@ -229,12 +307,14 @@ def test_wide_encode_batch_scattered(fam, mem):
     c.close()
 
 
+@pytest.mark.parametrize("cs", [1024, 1032])
 @pytest.mark.parametrize("mem", ["device", "host"])
 @pytest.mark.parametrize("fam", FAMS)
-def test_wide_decode_batch_mixed_patterns(fam, mem):
+def test_wide_decode_batch_mixed_patterns(fam, mem, cs):
     """mec_decode_batch, RS/CRS(8,6): every stripe its own pattern of 0..6
-    erasures (and some with 7: too many), random non-codeword stripes."""
-    k, m, cs, n = 8, 6, 1024, 40
+    erasures (and some with 7: too many), random non-codeword stripes;
+    cs = 1032: the per-row-group tail launches (8-byte tail)."""
+    k, m, n = 8, 6, 40
     if fam == "cauchy" and not ok_shape(fam, k, m, cs):
         pytest.skip("no Cauchy w")
     rng = np.random.default_rng(23)

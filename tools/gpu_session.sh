@@ -40,6 +40,10 @@ for step in "$@"; do
                 i=$((i + 1))
                 run "pytest_sel_$i" 600 python -u -m pytest $(echo "$grp" | tr '+' ' ') -m gpu -x -v --timeout 120 --timeout-method thread
             done ;;
+        bounds)  # the bounds-checked build (make -C memec_amd bounds) under the index-heavy suites
+            run pytest_bounds 900 env MEMEC_LIBMEC=memec_amd/bounds/libmec.so python -u -m pytest tests/test_gpu_wide.py \
+                tests/test_gpu_batch.py tests/test_gpu_sweep.py tests/test_gpu_queue.py tests/test_gpu_launch_knobs.py \
+                -m gpu -x -q --timeout 120 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py ;;
         benchdec) run bench_rs_dec 400 python bench.py --config rs_dec ;;
