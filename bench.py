@@ -894,6 +894,44 @@ def measure_extra(name, strong_global, steps, rank, world, dev, dist, all_ranks_
     return res
 
 
+def memory_plan(config, stripes, world, rank0, extras, ceiling, strong=False):
+    """Device bytes each phase of this process holds at once (torch
+    tensors; libmec's own tables are KiBs), for `stripes` per rank of
+    `config`: the timed launch's buffers, the decode twin's stripe copy and
+    saved erasures, rank 0's live reference streams (3 x 8 GiB of mec_xor
+    buffers), and each extra config beside the main buffers (which stay
+    allocated).  The driver's 8-GPU line runs one rank per GPU, so its peak
+    must fit one device."""
+    fam, k, m, cs, _, op, erased = CONFIGS[config]
+    S = stripes
+    phases = {}
+    if op == "encode":
+        base = (k + m) * cs * S
+        phases["timed"] = base
+        twin = {"rs_enc": "rs_dec", "crs_enc": "crs_dec", "rs42": "rs42_dec"}.get(config)
+        if twin:
+            e = len(CONFIGS[twin][6])
+            phases["decode_twin"] = base + (k + m) * cs * S + e * cs * S
+    elif op == "update":
+        base = (1 + m) * cs * S
+        phases["timed"] = base + (k + m) * cs * min(S, 256)
+    else:
+        base = (k + m) * cs * S + len(erased) * cs * S  # stripes + saved erasures
+        phases["timed"] = base + k * cs * S  # the data copy while the stripes are built
+    if ceiling and rank0:
+        phases["reference_streams"] = base + 3 * (8 << 30)
+    if extras:
+        for label, name, strong_global in EXTRA_CONFIGS:
+            _, k2, m2, cs2, s2, _, _ = CONFIGS[name]
+            if strong_global:
+                s2 = strong_global // world + (1 if strong_global % world else 0)
+            twin2 = DECODE_TWINS.get(name)
+            n = s2 if twin2 else min(s2, 4096)
+            e2 = len(CONFIGS[twin2][6]) if twin2 else m2
+            phases[label] = base + (k2 + m2) * cs2 * s2 + (k2 + m2) * cs2 * n + e2 * cs2 * n
+    return {"peak_bytes": max(phases.values()), "phases": phases}
+
+
 def runs_cpu_legs(rank, world, disabled):
     """Whether this rank times the reference CPU path (cpu_baseline, the
     decode twin's baseline, configs[0]'s reference_cpu): rank 0 at every N —
@@ -1202,6 +1240,27 @@ def main():
                          "registered": "mec_host_register: kernel reads/writes host memory over PCIe (zero-copy)"},
                **res}
 
+    # device memory: this run's measured peak on every rank against the plan
+    # for this run and for the full-size line with one rank per GPU
+    peak = int(torch.cuda.max_memory_allocated(dev))
+    peaks = [peak]
+    if use_pg:
+        peaks = [None] * world
+        dist.all_gather_object(peaks, peak)
+    with_extras = extras is not None
+    mem_plan = None
+    if rank == 0:
+        full_cfg = CONFIGS[args.config][4]
+        mem_plan = {
+            "device_bytes": int(torch.cuda.mem_get_info(dev)[1]),
+            "measured_peak_bytes_per_rank": peaks,
+            "this_run": memory_plan(args.config, stripes, world, True, with_extras, not args.no_ceiling, args.strong),
+            "full_size_one_rank_per_gpu": dict(
+                memory_plan(args.config, full_cfg, world, True, args.config == "rs_enc", True),
+                stripes_per_gpu=full_cfg, world=world),
+        }
+        mem_plan["full_size_fits"] = mem_plan["full_size_one_rank_per_gpu"]["peak_bytes"] <= mem_plan["device_bytes"]
+
     # every rank's GPU work (timed legs, pins, verifications) ends here; the
     # CPU legs below run on rank 0 alone, outside every timed region, while
     # the other ranks leave (a rank parked in an RCCL barrier would spin a
@@ -1267,6 +1326,7 @@ def main():
             line["decode_verified" if op == "decode" else "update_verified"] = ok
         if dist_info:
             line["dist"] = dist_info
+        line["memory_plan"] = mem_plan
         line["box"] = box_info(dev)
         if e2e:
             line["e2e_host_memory"] = e2e

@@ -125,6 +125,14 @@ typedef struct {
     uint64_t mg_cache_bytes;
     uint64_t mg_cache_tables;
     uint64_t mg_cache_uncached;
+    /* wide codes' run-time compiled bit-sliced kernels (MEC_BITSLICE): built,
+     * failed (those matrices stay on the one-pass kernel), still compiling,
+     * total compile milliseconds, and launches that ran one (ABI 5) */
+    uint64_t jit_kernels;
+    uint64_t jit_failed;
+    uint64_t jit_pending;
+    uint64_t jit_compile_ms;
+    uint64_t jit_launches;
 } mec_stats;
 
 typedef struct {
@@ -374,7 +382,7 @@ int mec_set_probe(mec_ctx *ctx, int mode);
 
 /* Launch-shape experiment overrides.  libmec reads MEC_SGROUP, MEC_WINDOWS,
  * MEC_BLOCK, MEC_GBLOCK, MEC_GWPC, MEC_BM_VW, MEC_WPC, MEC_COPY_THREADS, MEC_WIDE,
- * MEC_MG_ROWS from the environment once, at first use, never on a launch path; this
+ * MEC_MG_ROWS, MEC_BITSLICE from the environment once, at first use, never on a launch path; this
  * call changes one at run time (same name and value syntax as the
  * variable; value NULL = unset, i.e. the built-in rule).  Each stored
  * value is one atomic word, so a concurrent launch sees the old or the new

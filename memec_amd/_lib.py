@@ -46,7 +46,9 @@ class MecStats(ctypes.Structure):
                 ("queue_launches", ctypes.c_uint64), ("queue_slots", ctypes.c_uint32),
                 ("queue_parts", ctypes.c_uint32), ("queue_broken", ctypes.c_uint32), ("queue_devslot", ctypes.c_uint32),
                 ("queue_timeouts", ctypes.c_uint64), ("mg_cache_bytes", ctypes.c_uint64),
-                ("mg_cache_tables", ctypes.c_uint64), ("mg_cache_uncached", ctypes.c_uint64)]
+                ("mg_cache_tables", ctypes.c_uint64), ("mg_cache_uncached", ctypes.c_uint64),
+                ("jit_kernels", ctypes.c_uint64), ("jit_failed", ctypes.c_uint64), ("jit_pending", ctypes.c_uint64),
+                ("jit_compile_ms", ctypes.c_uint64), ("jit_launches", ctypes.c_uint64)]
 
 
 _lib = None

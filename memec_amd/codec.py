@@ -213,7 +213,9 @@ class Codec:
                 "queue_launches": st.queue_launches, "queue_slots": st.queue_slots,
                 "queue_parts": st.queue_parts, "queue_broken": bool(st.queue_broken), "queue_devslot": bool(st.queue_devslot),
                 "queue_timeouts": st.queue_timeouts, "mg_cache_bytes": st.mg_cache_bytes,
-                "mg_cache_tables": st.mg_cache_tables, "mg_cache_uncached": st.mg_cache_uncached}
+                "mg_cache_tables": st.mg_cache_tables, "mg_cache_uncached": st.mg_cache_uncached,
+                "jit_kernels": st.jit_kernels, "jit_failed": st.jit_failed, "jit_pending": st.jit_pending,
+                "jit_compile_ms": st.jit_compile_ms, "jit_launches": st.jit_launches}
 
 
 def fill_random(t, seed, word_offset=0, stream=None):

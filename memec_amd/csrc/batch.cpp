@@ -335,6 +335,22 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
         // (gf8_kernel / bm_kernel gather mode), only the pointers are read
         const std::vector<uint8_t> &ss = M.ssel[0], &ds = M.dsel[0];
         const Mat &cf = M.coef[0];
+        if (one_pass && jit_wanted(c, ds.size())) {
+            if (JitKernel *jk = jit_kernel(c, cf, ds.size(), M.K, M.accumulate, true)) {
+                BsLaunch L{};
+                L.stab = dstab;
+                L.dtab = ddtab;
+                L.sstride = sstride;
+                L.dstride = dstride;
+                L.k = int(M.K);
+                L.rows = int(ds.size());
+                L.len = c->cs;
+                L.n_stripes = n;
+                for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
+                for (size_t r = 0; r < ds.size(); ++r) L.dst_off[r] = ds[r];
+                return jit_launch(c, jk, L, st);
+            }
+        }
         if (one_pass) {
             Gf8MgLaunch L{};
             L.stab = dstab;
@@ -975,6 +991,14 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
         out->mg_cache_tables = c->mg.map.size();
         out->mg_cache_uncached = c->mg.uncached;
     }
+    {
+        std::lock_guard<std::mutex> jk(c->jit.mu);
+        out->jit_kernels = c->jit.ready;
+        out->jit_failed = c->jit.failed;
+        out->jit_pending = c->jit.pending;
+        out->jit_compile_ms = uint64_t(c->jit.compile_ms + 0.5);
+        out->jit_launches = c->jit.launches.load();
+    }
     for (mec_ctx *sc : c->shards) {  // a multi context reports its shards' sums
         mec_stats t{};
         (void)mec_get_stats(sc, &t);
@@ -993,6 +1017,11 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
         out->mg_cache_bytes += t.mg_cache_bytes;
         out->mg_cache_tables += t.mg_cache_tables;
         out->mg_cache_uncached += t.mg_cache_uncached;
+        out->jit_kernels += t.jit_kernels;
+        out->jit_failed += t.jit_failed;
+        out->jit_pending += t.jit_pending;
+        out->jit_compile_ms += t.jit_compile_ms;
+        out->jit_launches += t.jit_launches;
     }
     return MEC_OK;
 }

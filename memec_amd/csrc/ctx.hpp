@@ -173,6 +173,25 @@ struct MgCache {
 };
 constexpr size_t kMgBlock = size_t(4) << 20;
 
+// Run-time compiled bit-sliced kernels of wide matrices (jit.cpp).
+struct JitKernel {
+    std::atomic<int> state{0};  // 0 compiling, 1 ready, -1 failed
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    double compile_ms = 0;
+    std::string err;
+};
+struct JitCache {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::unordered_map<std::string, std::shared_ptr<JitKernel>> map;
+    size_t cap = 512;
+    uint32_t pending = 0;
+    uint64_t ready = 0, failed = 0;
+    double compile_ms = 0;
+    std::atomic<uint64_t> launches{0};
+};
+
 // Grid-wide control words, after the slots in the same mapped allocation.
 enum : uint32_t { kQCtlStop = 0, kQCtlExit = 1, kQCtlWords = 2 };
 struct HostQueue {
@@ -236,6 +255,8 @@ struct mec_ctx {
     // (gf8_mg_kernel), keyed by (rows, k, rows per group, coefficient
     // bytes); bounded (mec.cpp mg_tables)
     mec::core::MgCache mg;
+    // bit-sliced kernels compiled for this context's wide matrices
+    mec::core::JitCache jit;
 
     bool byte_wise() const { return family != MEC_CAUCHY_GOOD; }
     mec::Scheme scheme() const {
@@ -292,6 +313,14 @@ void bit_block(const Field &f, unsigned e, uint32_t w, uint8_t *mask, size_t mst
 constexpr int kMgUncached = 1;
 int mg_prepare(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, Gf8MgLaunch &L, hipStream_t stream);
 void mg_release(mec_ctx *c);
+// jit.cpp: wide byte-wise outputs through a run-time compiled bit-sliced
+// kernel.  jit_kernel: the kernel for this matrix, or nullptr (compiling,
+// failed, capped, MEC_BITSLICE=0) — the caller then runs gf8_mg_kernel.
+bool jit_wanted(const mec_ctx *c, size_t nd);
+JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool accumulate, bool gather);
+int jit_launch(mec_ctx *c, JitKernel *k, const BsLaunch &L, hipStream_t stream);
+void jit_init(mec_ctx *c);
+void jit_release(mec_ctx *c);
 // Byte-wise outputs beyond 4 per launch go through gf8_mg_kernel (every
 // source read once) unless MEC_WIDE=0 or the chunk has a sub-16-byte tail.
 bool mg_wanted(const mec_ctx *c, size_t nd);

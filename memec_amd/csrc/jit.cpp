@@ -1,0 +1,220 @@
+// jit.cpp — run-time compiled bit-sliced kernels for wide byte-wise codes
+// (more than 4 outputs: m > 4 encodes and updates, decodes of > 4 erasures).
+//
+// Each distinct coefficient matrix gets its own straight-line kernel
+// (bitslice.cpp: 8 x 8 bit transposes and a four-Russians XOR program with
+// the matrix baked in as constants), compiled with hiprtc for gfx950 and
+// loaded as a module on the context's device.  Compilation takes ~1 s, so by
+// default it runs on a background thread (MEC_BITSLICE=1) while the matrix's
+// calls keep running on gf8_mg_kernel; once the module is loaded every later
+// call with that matrix launches it.  MEC_BITSLICE=2 compiles on the calling
+// thread at first use (benchmarks, tests), 0 never uses it.  At most
+// MEC_JIT_MAX_KERNELS (default 512) matrices per context are compiled;
+// beyond that the one-pass kernel serves them.
+#include <hip/hiprtc.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <thread>
+
+#include "bitslice.hpp"
+#include "ctx.hpp"
+#include "knobs.hpp"
+#include "launch_plan.hpp"
+
+namespace mec {
+namespace core {
+namespace {
+
+// One background compiler thread per process, FIFO.
+struct Worker {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::function<void()>> jobs;
+    bool started = false;
+    void post(std::function<void()> f) {
+        std::lock_guard<std::mutex> g(mu);
+        jobs.push_back(std::move(f));
+        if (!started) {
+            started = true;
+            std::thread([this] {
+                for (;;) {
+                    std::function<void()> f;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [&] { return !jobs.empty(); });
+                        f = std::move(jobs.front());
+                        jobs.pop_front();
+                    }
+                    f();
+                }
+            }).detach();
+        }
+        cv.notify_one();
+    }
+};
+Worker &worker() {
+    static Worker *w = new Worker;  // never destroyed: the detached thread may outlive static destruction
+    return *w;
+}
+
+// hiprtc source -> gfx950 code object -> module on `device`.
+void compile(JitKernel &k, const std::string &src, int device) {
+    const auto t0 = std::chrono::steady_clock::now();
+    hiprtcProgram prog = nullptr;
+    std::string err;
+    std::vector<char> code;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "mec_bs.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        err = "hiprtcCreateProgram";
+    } else {
+        const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+        const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
+        if (r != HIPRTC_SUCCESS) {
+            size_t n = 0;
+            hiprtcGetProgramLogSize(prog, &n);
+            std::string log(n, '\0');
+            if (n) hiprtcGetProgramLog(prog, &log[0]);
+            err = std::string("hiprtc: ") + hiprtcGetErrorString(r) + ": " + log.substr(0, 400);
+        } else {
+            size_t n = 0;
+            hiprtcGetCodeSize(prog, &n);
+            code.resize(n);
+            hiprtcGetCode(prog, code.data());
+        }
+        hiprtcDestroyProgram(&prog);
+    }
+    if (err.empty()) {
+        DeviceGuard dg(device);
+        hipError_t e = hipModuleLoadData(&k.mod, code.data());
+        if (e == hipSuccess) e = hipModuleGetFunction(&k.fn, k.mod, "mec_bs");
+        if (e != hipSuccess) err = std::string("module: ") + hipGetErrorString(e);
+    }
+    k.compile_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    k.err = err;
+    k.state.store(err.empty() ? 1 : -1, std::memory_order_release);
+    if (!err.empty()) std::fprintf(stderr, "libmec: bit-sliced kernel not built (%s); gf8_mg_kernel serves it\n", err.c_str());
+}
+
+uint64_t env_u64(const char *name, uint64_t dflt) {
+    const char *e = std::getenv(name);
+    return e && *e ? std::strtoull(e, nullptr, 10) : dflt;
+}
+
+}  // namespace
+
+bool jit_wanted(const mec_ctx *c, size_t nd) {
+    const int64_t kn = detail::knob(detail::kKnobBitslice);
+    return kn != 0 && c->byte_wise() && nd > size_t(kMaxRows) && c->cs % 16 == 0;
+}
+
+// The kernel for (coef, accumulate, addressing), compiling it if needed;
+// nullptr while it compiles (async), past the cap, or after a failure.
+JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool accumulate, bool gather) {
+    std::string key(reinterpret_cast<const char *>(coef.data()), nd * ns);
+    key += char(nd);
+    key += char(ns);
+    key += char(accumulate ? 1 : 0);
+    key += char(gather ? 1 : 0);
+    JitCache &J = c->jit;
+    const bool sync = detail::knob(detail::kKnobBitslice) == 2;
+    std::shared_ptr<JitKernel> k;
+    bool fresh = false;
+    {
+        std::unique_lock<std::mutex> g(J.mu);
+        auto it = J.map.find(key);
+        if (it != J.map.end()) {
+            k = it->second;
+        } else {
+            if (J.map.size() >= J.cap) return nullptr;
+            k = std::make_shared<JitKernel>();
+            J.map.emplace(key, k);
+            fresh = true;
+            ++J.pending;
+        }
+    }
+    if (fresh) {
+        auto src = std::make_shared<std::string>(bs_source(bs_build(coef.data(), int(nd), int(ns), accumulate), gather));
+        const int device = c->device;
+        auto done = [&J, k] {
+            std::lock_guard<std::mutex> g(J.mu);
+            --J.pending;
+            J.compile_ms += k->compile_ms;
+            if (k->state.load() > 0) ++J.ready;
+            else ++J.failed;
+            J.cv.notify_all();
+        };
+        if (sync) {
+            compile(*k, *src, device);
+            done();
+        } else {
+            worker().post([k, src, device, done] {
+                compile(*k, *src, device);
+                done();
+            });
+        }
+    }
+    if (sync && k->state.load(std::memory_order_acquire) == 0) {  // another thread compiling it: wait
+        std::unique_lock<std::mutex> g(J.mu);
+        J.cv.wait(g, [&] { return k->state.load(std::memory_order_acquire) != 0; });
+    }
+    return k->state.load(std::memory_order_acquire) > 0 ? k.get() : nullptr;
+}
+
+int jit_launch(mec_ctx *c, JitKernel *k, const BsLaunch &L, hipStream_t stream) {
+    BsParams p{};
+    p.src = L.src;
+    p.dst = L.dst;
+    p.sss = L.src_stripe_stride;
+    p.dss = L.dst_stripe_stride;
+    p.stab = L.stab;
+    p.dtab = L.dtab;
+    p.sstride = L.sstride;
+    p.dstride = L.dstride;
+    p.chunk = uint32_t(L.len);
+    for (int j = 0; j < L.k; ++j) p.src_off[j] = L.src_off[j];
+    for (int r = 0; r < L.rows; ++r) p.dst_off[r] = L.dst_off[r];
+    for (uint32_t s0 = 0; s0 < L.n_stripes;) {
+        const detail::KernelPlan pl = detail::plan_bs(L, s0);
+        if (!pl.ok) return fail(MEC_EINVAL, "bit-sliced launch: %s", pl.why);
+        p.tiles = pl.geo.tiles;
+        p.nstr = pl.ns;
+        p.win = pl.win;
+        p.s0 = s0;
+        if (!L.stab) {
+            p.src = L.src + int64_t(s0) * L.src_stripe_stride;
+            p.dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+        }
+        size_t sz = sizeof(p);
+        void *cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &p, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+        HIP_TRY(hipModuleLaunchKernel(k->fn, uint32_t(pl.grid), 1, 1, pl.bt, 1, 1, pl.lds_dynamic, stream, nullptr, cfg));
+        s0 += pl.ns;
+    }
+    c->jit.launches.fetch_add(1, std::memory_order_relaxed);
+    return MEC_OK;
+}
+
+void jit_init(mec_ctx *c) { c->jit.cap = size_t(env_u64("MEC_JIT_MAX_KERNELS", 512)); }
+
+void jit_release(mec_ctx *c) {
+    JitCache &J = c->jit;
+    {
+        std::unique_lock<std::mutex> g(J.mu);
+        J.cv.wait(g, [&] { return J.pending == 0; });
+    }
+    bool any = false;
+    for (auto &kv : J.map) any = any || kv.second->mod;
+    if (any) {
+        DeviceGuard dg(c->device);
+        (void)hipDeviceSynchronize();  // no launch of a module may still run
+        for (auto &kv : J.map)
+            if (kv.second->mod) (void)hipModuleUnload(kv.second->mod);
+    }
+    J.map.clear();
+}
+
+}  // namespace core
+}  // namespace mec

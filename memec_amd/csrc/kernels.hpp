@@ -149,6 +149,22 @@ inline int gf8_mg_rows(int rows, int k, bool vand) {
 // R x k x 8 dwords, padding rows zero.
 void gf8_mg_tables(const uint8_t *coef, int rows, int k, int R, std::vector<uint32_t> &out);
 
+// Run-time compiled bit-sliced launch (jit.cpp, bitslice.hpp): rows > 4
+// byte-wise outputs of a chunk that is a multiple of 16 bytes, strided or
+// gathered addressing as Gf8MgLaunch.
+struct BsLaunch {
+    const uint8_t *src;
+    uint8_t *dst;
+    int64_t src_stripe_stride, dst_stripe_stride;
+    const uint64_t *stab, *dtab;
+    uint32_t sstride, dstride;
+    int64_t src_off[kMaxSrc];
+    int64_t dst_off[kMaxSrc];
+    int k, rows;
+    uint64_t len;
+    uint32_t n_stripes;
+};
+
 hipError_t launch_gf8(const Gf8Launch &L, hipStream_t stream);
 hipError_t launch_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream);
 hipError_t launch_gf8_gather(const GatherLaunch &L, hipStream_t stream);

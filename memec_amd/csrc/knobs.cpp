@@ -26,6 +26,7 @@ constexpr KnobSpec kSpecs[] = {
     {"MEC_COPY_THREADS", kKnobCopyThreads, 1, 64, {}, 0},
     {"MEC_WIDE", kKnobWide, 0, 1, {}, 0},
     {"MEC_MG_ROWS", kKnobMgRows, 3, 8, {3, 4, 8}, 3},
+    {"MEC_BITSLICE", kKnobBitslice, 0, 2, {}, 0},
 };
 // every knob but MEC_SGROUP's run half has its own variable
 static_assert(sizeof(kSpecs) / sizeof(kSpecs[0]) == kKnobCount - 1, "a knob whose variable is never read");

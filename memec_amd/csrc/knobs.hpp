@@ -32,6 +32,7 @@ enum Knob : int {
     kKnobCopyThreads, // MEC_COPY_THREADS=<n>
     kKnobWide,        // MEC_WIDE=0: > 4 outputs as 4-row launches (A/B of gf8_mg_kernel)
     kKnobMgRows,      // MEC_MG_ROWS=3|4|8: rows per group of gf8_mg_kernel
+    kKnobBitslice,    // MEC_BITSLICE=0|1|2: wide codes' run-time compiled kernels off / async (default) / sync
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

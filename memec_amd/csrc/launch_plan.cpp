@@ -372,6 +372,31 @@ KernelPlan plan_bm_gather(const GatherLaunch &L, uint32_t s0) {
     return p;
 }
 
+KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
+    KernelPlan p;
+    p.k = L.k;
+    p.rows = L.rows;
+    if (L.k < 1 || L.rows <= kMaxRows || L.k + L.rows > kMaxSrc) return fail_plan(p, "bit-sliced launches take 5..31 rows"), p;
+    if (L.len == 0 || L.len % 16 || L.len > (uint64_t(1) << 32) - 2048) return fail_plan(p, "chunk size"), p;
+    p.bt = kWaveBlock;
+    // 2 KiB per block: each lane two 16-byte units 1 KiB apart
+    p.geo.units = uint32_t(L.len / 16);
+    p.geo.tiles = uint32_t((L.len + 2047) / 2048);
+    p.geo.max_stripes_per_launch = std::max<uint32_t>(1, uint32_t(((uint64_t(1) << 31) / kWaveBlock) / p.geo.tiles));
+    p.ns = sub_stripes(p.geo, L.n_stripes, s0);
+    p.grid = uint64_t(p.ns) * p.geo.tiles;
+    if (!L.stab) {
+        const uint8_t *src = L.src + int64_t(s0) * L.src_stripe_stride;
+        const uint8_t *dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
+        p.win = launch_windows(src, int64_t(p.ns) * L.src_stripe_stride, dst, int64_t(p.ns) * L.dst_stripe_stride);
+    }
+    // occupancy is the program's VGPRs (~190 for 16 sources x 8 rows); only
+    // a forced MEC_WPC caps it
+    p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0, 0);
+    common_ok(p, uint64_t(p.geo.tiles) * 2048);
+    return p;
+}
+
 KernelPlan plan_xor(uint64_t len) {
     KernelPlan p;
     // one-wave blocks over 1 KiB tiles unless MEC_BLOCK=256, like the

@@ -181,6 +181,9 @@ KernelPlan plan_bm(const BmLaunch &L, uint32_t s0);
 // gf8_gather_kernel / bm_gather_kernel (one launch per max_stripes chunk).
 KernelPlan plan_gf8_gather(const GatherLaunch &L, uint32_t s0);
 KernelPlan plan_bm_gather(const GatherLaunch &L, uint32_t s0);
+// The run-time compiled bit-sliced kernel (jit.cpp): one-wave blocks over
+// 2 KiB tiles of every chunk.
+KernelPlan plan_bs(const BsLaunch &L, uint32_t s0);
 // xor_kernel over len bytes.
 KernelPlan plan_xor(uint64_t len);
 

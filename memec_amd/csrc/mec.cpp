@@ -148,6 +148,23 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
         return MEC_OK;
     }
     const bool probe = c->probe.load(std::memory_order_relaxed) == MEC_PROBE_XOR;
+    if (!probe && jit_wanted(c, nd)) {
+        // more than 4 outputs: the matrix's own bit-sliced kernel once built
+        if (JitKernel *jk = jit_kernel(c, coef, nd, ns, accumulate, false)) {
+            mec::BsLaunch L{};
+            L.src = lay.src;
+            L.dst = lay.dst;
+            L.src_stripe_stride = lay.sss;
+            L.dst_stripe_stride = lay.dss;
+            L.k = int(ns);
+            L.rows = int(nd);
+            L.len = c->cs;
+            L.n_stripes = n_stripes;
+            for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
+            for (size_t r = 0; r < nd; ++r) L.dst_off[r] = lay.dst_off[r];
+            return jit_launch(c, jk, L, stream);
+        }
+    }
     if (mg_wanted(c, nd) && !probe) {
         // more than 4 outputs: one pass over the sources (gf8_mg_kernel)
         mec::Gf8MgLaunch L{};
@@ -426,6 +443,7 @@ int mec_create(int family, uint32_t k, uint32_t m, uint32_t chunk_size, int devi
             break;
     }
     c->packet = family == MEC_CAUCHY_GOOD ? chunk_size / c->w : chunk_size;
+    jit_init(c.get());
     {  // one-pass table cache cap (read here, never on a launch path)
         const char *e = std::getenv("MEC_MG_CACHE_BYTES");
         c->mg.cap = e && *e ? size_t(std::strtoull(e, nullptr, 10)) : (size_t(64) << 20);
@@ -471,6 +489,7 @@ void mec_destroy(mec_ctx *c) {
             }
             if (c->bdev[i]) (void)hipFree(c->bdev[i]);
         }
+        jit_release(c);
         mg_release(c);
     }
     delete c;

@@ -1,0 +1,68 @@
+// bitslice_check.cc — CPU check of the bit-sliced GF(2^8) programs
+// (memec_amd/csrc/bitslice.cpp) before any device runs one: for random and
+// structured coefficient matrices of every wide shape (5..31 outputs, k + m
+// <= 32), the program interpreted over random 32-byte chunks equals the
+// byte-wise GF(2^8) products (0x11d), overwrite and accumulate; the emitted
+// HIP source is generated for each.  Prints "ok <programs> <ops>".
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "bitslice.hpp"
+#include "gf_math.hpp"
+
+using namespace mec;
+
+int main() {
+    const Field &f = Field::get(8);
+    std::mt19937_64 rng(12345);
+    long programs = 0, ops = 0;
+    for (int nd = 1; nd <= 31; ++nd)
+        for (int ns = 1; ns + nd <= 32; ++ns)
+            for (int kind = 0; kind < 3; ++kind)
+                for (int acc = 0; acc < 2; ++acc) {
+                    std::vector<uint8_t> coef(size_t(nd) * ns);
+                    for (size_t i = 0; i < coef.size(); ++i) {
+                        const uint8_t c = uint8_t(rng());
+                        // kind 1: Vandermonde-like ones in row 0 / column 0; kind 2: sparse with zeros
+                        coef[i] = kind == 1 && (i < size_t(ns) || i % size_t(ns) == 0) ? 1 : kind == 2 && (c & 3) == 0 ? 0 : c;
+                    }
+                    BsProgram p = bs_build(coef.data(), nd, ns, acc != 0);
+                    for (int trial = 0; trial < 3; ++trial) {
+                        std::vector<std::vector<uint8_t>> src(size_t(ns), std::vector<uint8_t>(32)),
+                            out(size_t(nd), std::vector<uint8_t>(32));
+                        std::vector<const uint8_t *> sp;
+                        std::vector<uint8_t *> op;
+                        for (auto &c : src) {
+                            for (auto &b : c) b = uint8_t(rng());
+                            sp.push_back(c.data());
+                        }
+                        for (auto &c : out) {
+                            for (auto &b : c) b = uint8_t(rng());
+                            op.push_back(c.data());
+                        }
+                        std::vector<std::vector<uint8_t>> want = out;
+                        for (int r = 0; r < nd; ++r)
+                            for (int b = 0; b < 32; ++b) {
+                                uint8_t x = acc ? want[size_t(r)][size_t(b)] : 0;
+                                for (int j = 0; j < ns; ++j) x ^= f.mul(coef[size_t(r) * ns + j], src[size_t(j)][size_t(b)]);
+                                want[size_t(r)][size_t(b)] = x;
+                            }
+                        bs_run(p, sp.data(), op.data());
+                        if (out != want) {
+                            std::printf("MISMATCH nd=%d ns=%d kind=%d acc=%d trial=%d\n", nd, ns, kind, acc, trial);
+                            return 1;
+                        }
+                    }
+                    if (nd >= 5 && kind == 0 && acc == 0 && (ns == 16 || ns == 12) && nd == 8)
+                        std::printf("shape %dx%d: %zu ops (transpose %u, combine %u, accumulate %u), source %zu bytes\n", nd,
+                                    ns, p.ops.size(), p.n_transpose, p.n_combine, p.n_accumulate, bs_source(p, false).size());
+                    (void)bs_source(p, (programs & 1) != 0);
+                    ++programs;
+                    ops += long(p.ops.size());
+                }
+    std::printf("ok %ld %ld\n", programs, ops);
+    return 0;
+}

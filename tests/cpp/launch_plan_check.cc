@@ -160,6 +160,38 @@ static void check_mg(int k, int rows, uint64_t chunk, uint32_t n, bool in_place,
     }
 }
 
+static void check_bs(int k, int rows, uint64_t chunk, uint32_t n, bool in_place, bool gather) {
+    BsLaunch L{};
+    const Layout ly = layout(in_place, chunk, k, rows);
+    L.src = ly.src;
+    L.dst = ly.dst;
+    L.src_stripe_stride = ly.sss;
+    L.dst_stripe_stride = ly.dss;
+    static const uint64_t tab[1] = {0};
+    if (gather) {
+        L.stab = L.dtab = tab;
+        L.sstride = L.dstride = uint32_t(k + rows);
+    }
+    L.k = k;
+    L.rows = rows;
+    L.len = chunk;
+    L.n_stripes = n;
+    uint64_t covered = 0;
+    for (uint32_t s0 = 0; s0 < n;) {
+        const KernelPlan p = plan_bs(L, s0);
+        common(p, uint64_t(p.geo.tiles) * 2048);
+        if (!p.ok || p.ns == 0) break;
+        if (p.bt != uint32_t(kWaveBlock)) bad("bit-sliced kernels are one-wave blocks", p);
+        if (uint64_t(p.geo.tiles) * 2048 < chunk) bad("tiles do not cover the chunk", p);
+        covered += p.ns;
+        s0 += p.ns;
+    }
+    if (covered != n) {
+        KernelPlan z;
+        bad("sub-launches do not cover the batch", z);
+    }
+}
+
 static void check_bm(int k, int rows, int w, uint64_t packet, uint32_t n, bool in_place, bool acc, bool gather) {
     BmLaunch L{};
     const Layout ly = layout(in_place, packet * uint64_t(w), k, rows);
@@ -237,6 +269,7 @@ static void sweep() {
                         }
                         if (chunk % 16 == 0)
                             for (int rows = kMaxRows + 1; k + rows <= kMaxSrc; ++rows) {
+                                if (vand) check_bs(k, rows, chunk, n, ip, rows % 2 == 0);
                                 check_mg(k, rows, chunk, n, ip, vand, false, false);
                                 check_mg(k, rows, chunk, n, ip, vand, true, false);
                                 check_mg(k, rows, chunk, n, ip, vand, false, true);

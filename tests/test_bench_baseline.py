@@ -217,3 +217,18 @@ def test_reference_decode_leg_fewer_codewords_than_sample(monkeypatch):
     r = bench.cpu_baseline_reference("rs", k, m, cs, None, 0, 16, "decode", [0, 1, 2, 3], cw)
     assert r["kind"] == "reference" and r["matches_gpu"] is True
     assert r["sample"].startswith("8 stripes")
+
+
+def test_memory_plan_full_size_fits_one_mi355x():
+    """bench.memory_plan: the default line (configs[1] with its decode twin,
+    rank 0's 3 x 8 GiB reference streams, configs[0]/[3]/[4] beside it) at
+    full size, one rank per GPU at 1..8 ranks, peaks at 128 GiB — under one
+    MI355X's 288 GB; every timed config alone fits too."""
+    import bench
+    for world in (1, 2, 4, 8):
+        p = bench.memory_plan("rs_enc", 4096, world, True, True, True)
+        assert p["phases"]["timed"] == 56 << 30
+        assert p["phases"]["reference_streams"] == 80 << 30
+        assert p["peak_bytes"] == 128 << 30
+    for name, cfg in bench.CONFIGS.items():
+        assert bench.memory_plan(name, cfg[4], 1, True, False, True)["peak_bytes"] < 288e9 * 0.9, name

@@ -106,3 +106,41 @@ def test_bench_gpus4_carries_cpu_baseline():
     cb = rec["cpu_baseline"]
     assert cb["kind"] == "reference" and cb["matches_gpu"] is True and cb["cores"] >= 1, cb
     assert "rank 0 of 4" in cb["when"]
+
+
+@pytest.mark.timeout(900)
+def test_bench_gpus8_default_line_rehearsal():
+    """The driver's 8-GPU default line rehearsed with 8 gloo ranks sharing
+    the one GPU: world size 8; configs[4]'s 32768
+    stripes sharded 4096 per rank; every parity pin and verification true
+    on all 8 ranks; configs[0]'s reference leg and the reference CPU
+    baseline timed on rank 0 after the other 7 ranks left; and the line's
+    memory plan — with one rank per GPU at full size (56 GiB of configs[1]
+    buffers, the 128 GiB decode-twin phase, 24 GiB of mec_xor streams on
+    rank 0) — fits one device, the plan agreeing with the measured peak of
+    this run on every rank."""
+    rec = _run("--stripes", "64", "--extra-configs", gpus=8)
+    assert rec["n_gpus"] == 8 and rec["dist"]["world_size"] == 8 and len(rec["dist"]["rank_devices"]) == 8
+    assert rec["config"]["global_stripes"] == 8 * 64
+    assert rec["parity"]["equal"] is True and rec["parity"]["ranks"] == 8
+    assert rec["decode"]["verified"] is True and rec["decode"]["parity"]["equal"] is True
+    oc = rec["other_configs"]
+    c0, c3, c4 = oc["configs[0]"], oc["configs[3]"], oc["configs[4]"]
+    assert c0["global_stripes"] == 8 * 65536 and c0["parity"]["equal"] is True and c0["decode"]["verified"] is True
+    assert c3["global_stripes"] == 8 * 65536 and c3["verified"] is True and c3["parity"]["equal"] is True
+    assert c4["scaling"] == "strong" and c4["stripes_per_gpu"] == 4096 and c4["global_stripes"] == 32768
+    assert c4["parity"]["equal"] is True and c4["parity"]["ranks"] == 8
+    assert c4["decode"]["verified"] is True and c4["decode"]["parity"]["equal"] is True
+    assert c0["reference_cpu"]["encode_matches_oracle"] is True and c0["reference_cpu"]["kind"] == "reference"
+    cb = rec["cpu_baseline"]
+    assert cb["kind"] == "reference" and cb["matches_gpu"] is True and "rank 0 of 8" in cb["when"], cb
+    assert rec["decode"]["cpu_baseline"]["kind"] == "reference"
+    mp = rec["memory_plan"]
+    full = mp["full_size_one_rank_per_gpu"]
+    assert full["world"] == 8 and full["stripes_per_gpu"] == 4096
+    assert full["phases"]["timed"] == 56 << 30 and full["phases"]["reference_streams"] == (56 + 24) << 30
+    assert full["peak_bytes"] <= mp["device_bytes"] and mp["full_size_fits"] is True, mp
+    plan = mp["this_run"]["peak_bytes"]
+    assert len(mp["measured_peak_bytes_per_rank"]) == 8
+    for got in mp["measured_peak_bytes_per_rank"]:
+        assert 0.5 * plan <= got <= 1.3 * plan + (256 << 20), (got, plan)

@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
-"""A/B of wide codes (m > 4): the one-pass multi-group kernel (gf8_mg_kernel,
-default) against 4-row launches that re-read the sources (MEC_WIDE=0).
+"""A/B of wide codes (m > 4) between kernel arms, interleaved in one
+process: "bs" the run-time compiled bit-sliced kernel (MEC_BITSLICE=2,
+compiled before timing), "mg" the one-pass multi-group kernel
+(gf8_mg_kernel, MEC_BITSLICE=0), "split" 4-row launches that re-read the
+sources (MEC_BITSLICE=0 MEC_WIDE=0).
 
-  python tools/wide_ab.py [--mode both|wide|split] [--steps N] [--pmc-out F]
+  python tools/wide_ab.py [--arms bs,mg] [--steps N] [--shape I]
 
 Every launch is checked against the other arm's parity (bit-exact), and the
 GPU time per step (HIP events around `steps` encodes / decodes) is printed
@@ -31,7 +34,11 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("rs", 10, 4, 1 << 20, 4096, "encode")]
 
 
-def run(mode, steps, warmup, shapes):
+ARMS = {"bs": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
+        "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"}}
+
+
+def run(arms_list, steps, warmup, shapes):
     import torch
     import memec_amd
     from memec_amd import Codec, fill_random
@@ -64,8 +71,9 @@ def run(mode, steps, warmup, shapes):
             alg = (k + m) * cs * n
             result = lambda: st[:, erased]  # noqa: E731
         arms = {}
-        for arm in (["wide", "split"] if mode == "both" else [mode]):
-            memec_amd.set_knob("MEC_WIDE", None if arm == "wide" else "0")
+        for arm in arms_list:
+            for kn in ("MEC_BITSLICE", "MEC_WIDE"):
+                memec_amd.set_knob(kn, ARMS[arm].get(kn))
             for _ in range(warmup):
                 step()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -78,12 +86,13 @@ def run(mode, steps, warmup, shapes):
             arms[arm] = {"ms_per_step": round(ms, 4), "GBps": round(alg / (ms * 1e-3) / 1e9, 1),
                          "frac": round(alg / (ms * 1e-3) / 8e12, 4)}
             arms[arm]["digest"] = int(result().view(torch.int64).sum().item())
-        memec_amd.set_knob("MEC_WIDE", None)
+        for kn in ("MEC_BITSLICE", "MEC_WIDE"):
+            memec_amd.set_knob(kn, None)
         rec = {"family": fam, "k": k, "m": m, "chunk": cs, "stripes": n, "op": op, "alg_bytes": alg, **arms}
         if op == "decode":
             rec["restored"] = bool(torch.equal(result(), orig))
-        if mode == "both":
-            rec["equal"] = arms["wide"]["digest"] == arms["split"]["digest"]
+        rec["equal"] = len({arms[a]["digest"] for a in arms_list}) == 1
+        rec["jit"] = {x: c.stats()[x] for x in ("jit_kernels", "jit_launches", "jit_compile_ms", "jit_failed")}
         print(json.dumps(rec), flush=True)
         out.append(rec)
         c.close()
@@ -100,7 +109,7 @@ def summarise(csv_path, counter, steps, warmup):
             if row["Counter_Name"] != counter:
                 continue
             name = row["Kernel_Name"]
-            if "gf8" in name or "bm_kernel" in name:
+            if "gf8" in name or "bm_kernel" in name or "mec_bs" in name:
                 tot += float(row["Counter_Value"])
                 n += 1
     return tot / (steps + warmup), n
@@ -108,7 +117,8 @@ def summarise(csv_path, counter, steps, warmup):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="both", choices=["both", "wide", "split"])
+    ap.add_argument("--arms", default="bs,mg", help="comma-separated arms of ARMS, timed in this order")
+    ap.add_argument("--rounds", type=int, default=1, help="repeat the whole shape list")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (default: all)")
@@ -122,9 +132,10 @@ if __name__ == "__main__":
         rd, wr = 2 * fk * 1024, wk * 1024
         alg_r = k * cs * n
         alg_w = m * cs * n
-        print(json.dumps({"shape": shapes[0], "mode": a.mode, "launch_rows": [nf, nw],
+        print(json.dumps({"shape": shapes[0], "arms": a.arms, "launch_rows": [nf, nw],
                           "read_bytes_per_step": rd, "write_bytes_per_step": wr,
                           "read_ratio": round(rd / alg_r, 4), "write_ratio": round(wr / alg_w, 4),
                           "traffic_ratio": round((rd + wr) / (alg_r + alg_w), 4)}))
     else:
-        run(a.mode, a.steps, a.warmup, shapes)
+        for _ in range(a.rounds):
+            run(a.arms.split(","), a.steps, a.warmup, shapes)
