@@ -33,7 +33,7 @@ struct Group {
     uint32_t n = 0;
     std::vector<uint64_t> ptrs;  // n rows of [ns sources | nd outputs]
     std::vector<int32_t> owner;  // per stripe: index of the request / stripe it came from
-    std::shared_ptr<LinearPlan> plan;  // decode groups: survivor / output chunk indices
+    const LinearPlan *plan = nullptr;  // decode groups: survivor / output chunk indices (owned by the context)
     std::vector<uint32_t> cols, rows;  // encode / update groups: source columns, output rows
 };
 
@@ -118,7 +118,7 @@ int add_decode(mec_ctx *c, GroupSet &G, uint8_t *const *chunks, uint64_t present
         if (!chunks[i]) return fail(MEC_EINVAL, "chunk %u pointer is NULL", i);
     auto it = G.index.find(present);
     if (it == G.index.end()) {
-        std::shared_ptr<LinearPlan> plan;
+        const LinearPlan *plan = nullptr;
         int rc = get_plan(c, present, plan);
         if (rc != MEC_OK) return rc;
         bool fresh;
@@ -727,10 +727,7 @@ int submit(mec_ctx *c, Request &req) {
     return req.rc;
 }
 
-bool coalescing(mec_ctx *c) {
-    std::lock_guard<std::mutex> lk(c->coal.mu);
-    return c->coal.max_batch > 0;
-}
+bool coalescing(mec_ctx *c) { return c->coal.max_batch.load(std::memory_order_relaxed) > 0; }
 
 int submit_encode(mec_ctx *c, const uint8_t *const *data, uint8_t *const *parity) {
     Request r{0, data, parity, 0, 0, nullptr};
@@ -875,7 +872,7 @@ int mec_decode_batch(mec_ctx *c, uint8_t *const *chunks, const uint64_t *present
                     if (present != last_mask) {
                         auto it = ids.find(present);
                         if (it == ids.end()) {
-                            std::shared_ptr<LinearPlan> plan;
+                            const LinearPlan *plan = nullptr;
                             src = get_plan(c, present, plan);
                             if (src == MEC_OK) {
                                 if (M.ssel.size() >= kSkipStripe) {
@@ -962,7 +959,7 @@ int mec_set_coalescing(mec_ctx *c, uint32_t max_batch) {
     CHECK_CTX(c);
     for (mec_ctx *sc : c->shards) (void)mec_set_coalescing(sc, max_batch);
     std::lock_guard<std::mutex> lk(c->coal.mu);
-    c->coal.max_batch = max_batch;
+    c->coal.max_batch.store(max_batch, std::memory_order_relaxed);
     return MEC_OK;
 }
 

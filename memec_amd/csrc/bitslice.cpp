@@ -178,10 +178,12 @@ void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out) 
     }
 }
 
-std::string bs_source(const BsProgram &p, bool gather) {
+std::string bs_source(const BsProgram &p, bool gather, int waves, int prefetch) {
     std::string s;
     s.reserve(p.ops.size() * 48 + 4096);
     s += gather ? "#define MEC_GATHER 1\n" : "#define MEC_GATHER 0\n";
+    if (waves > 0) s += "#define MEC_WAVES __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))\n";
+    else s += "#define MEC_WAVES\n";
     s += R"HIP(
 typedef unsigned int u32;
 typedef unsigned long long u64;
@@ -210,7 +212,7 @@ __device__ __forceinline__ void mec_st(u32 a, u32 b, u32 c, u32 d, __amdgpu_buff
 }
 #define BFI(m, a, b) ((u32)__builtin_amdgcn_bitop3_b32(m, a, b, 0xCA))
 #define X3(a, b, c) ((u32)__builtin_amdgcn_bitop3_b32(a, b, c, 0x96))
-extern "C" __global__ __launch_bounds__(64) void mec_bs(const BsParams p) {
+extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams p) {
     u32 bid = blockIdx.x;
     if (!MEC_GATHER && p.win > 1) {  // in-place layouts: windows taken round-robin (stream_common.hpp block_order)
         const u32 per = gridDim.x / p.win;
@@ -229,14 +231,19 @@ extern "C" __global__ __launch_bounds__(64) void mec_bs(const BsParams p) {
 #endif
 )HIP";
     char buf[320];
-    // source units: all loads first (the compiler keeps them in flight)
-    for (int j = 0; j < p.ns; ++j) {
+    // source units: the first `depth` sources' loads up front, then each
+    // further source's loads just before the combine of the source `depth`
+    // places earlier (depth 0: all loads first)
+    const int depth = prefetch > 0 && prefetch < p.ns ? prefetch : p.ns;
+    auto emit_load = [&](int j) {
         std::snprintf(buf, sizeof buf,
                       "    const __amdgpu_buffer_rsrc_t rs%d = mec_rsrc(src_at(%d), p.chunk);\n"
                       "    const u32x4 sa%d = LD(rs%d, off), sb%d = LD(rs%d, off + 1024u);\n",
                       j, j, j, j, j, j);
         s += buf;
-    }
+    };
+    for (int j = 0; j < depth; ++j) emit_load(j);
+    int next_load = depth;
     for (int r = 0; r < p.nd; ++r) {
         std::snprintf(buf, sizeof buf, "    const __amdgpu_buffer_rsrc_t rd%d = mec_rsrc(dst_at(%d), p.chunk);\n", r, r);
         s += buf;
@@ -251,6 +258,9 @@ extern "C" __global__ __launch_bounds__(64) void mec_bs(const BsParams p) {
     std::vector<std::vector<int>> stored(size_t(p.nd), std::vector<int>(8, -1));
     for (size_t i = 0; i < p.ops.size(); ++i) {
         const BsOp &o = p.ops[i];
+        if (o.op == BsOpc::kLoad && o.b == 0 && o.a > 0 && next_load < p.ns && next_load <= o.a + depth - 1) {
+            emit_load(next_load++);  // source o.a starts: keep `depth` sources in flight
+        }
         switch (o.op) {
             case BsOpc::kLoad:
                 std::snprintf(buf, sizeof buf, "    const u32 v%zu = s%c%d.%c;\n", i, o.b < 4 ? 'a' : 'b', o.a, comp[o.b & 3]);

@@ -65,7 +65,11 @@ BsProgram bs_build(const uint8_t *coef, int nd, int ns, bool accumulate);
 void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out);
 // HIP source of the kernel `mec_bs` (one-wave blocks, 2 KiB of every chunk
 // per block; strided or gathered addressing, BsParams below).
-std::string bs_source(const BsProgram &p, bool gather);
+// waves > 0: compiled for at least that many waves per SIMD
+// (amdgpu_waves_per_eu; the register budget shrinks accordingly).
+// prefetch > 0: at most that many sources' loads issued ahead of the
+// combine (0: every load first).
+std::string bs_source(const BsProgram &p, bool gather, int waves = 0, int prefetch = 0);
 
 // Kernel arguments of every generated kernel (the same layout in the
 // generated source, bs_source).  Strided: source j of stripe s at src + s *

@@ -101,7 +101,7 @@ struct Coalescer {
     std::condition_variable cv;
     std::deque<Request *> queue;
     uint32_t leaders = 0;    // batches in flight (at most kMaxLeaders)
-    uint32_t max_batch = 0;  // 0 = coalescing off
+    std::atomic<uint32_t> max_batch{0};  // 0 = coalescing off (read lock-free on every host call)
     uint64_t batches = 0, requests = 0;  // statistics
 };
 
@@ -228,6 +228,13 @@ struct mec_ctx {
     mec::Mat A;  // m x k (Jerasure) or (k+m) x k (ISA-L)
     std::mutex plan_mu;
     std::unordered_map<uint64_t, std::shared_ptr<mec::LinearPlan>> plans;
+    // lock-free index of `plans` for the per-call lookup (mec.cpp get_plan):
+    // open addressing on the present mask, entries only ever added (the
+    // plans live in `plans` until mec_destroy); a full table falls back to
+    // the mutex
+    static constexpr size_t kPlanSlots = 4096;
+    std::unique_ptr<std::atomic<uint64_t>[]> plan_keys{new std::atomic<uint64_t>[kPlanSlots]()};
+    std::unique_ptr<std::atomic<const mec::LinearPlan *>[]> plan_vals{new std::atomic<const mec::LinearPlan *>[kPlanSlots]()};
     std::mutex lane_mu;
     std::vector<mec::core::Lane *> lanes_free;
     std::vector<mec::core::Lane *> lanes_all;
@@ -330,7 +337,7 @@ int apply(mec_ctx *c, const uint8_t *src, int64_t sss, const std::vector<int64_t
           int64_t dss, const std::vector<int64_t> &dst_off, const Mat &coef, uint32_t n_stripes, bool accumulate,
           hipStream_t stream);
 // Cached decode plan for a present-chunk mask (reference survivor choice).
-int get_plan(mec_ctx *c, uint64_t present, std::shared_ptr<mec::LinearPlan> &out);
+int get_plan(mec_ctx *c, uint64_t present, const mec::LinearPlan *&out);  // owned by the context
 Mat encode_rows(const mec_ctx *c, const std::vector<uint32_t> &rows, const std::vector<uint32_t> &cols);
 std::vector<uint32_t> mask_rows(const mec_ctx *c, uint32_t parity_mask);
 Lane *lane_acquire(mec_ctx *c, int &rc);

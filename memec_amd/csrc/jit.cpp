@@ -119,6 +119,12 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     key += char(ns);
     key += char(accumulate ? 1 : 0);
     key += char(gather ? 1 : 0);
+    const int64_t wk = detail::knob(detail::kKnobBsWaves);  // experiments (mec_set_knob)
+    const int waves = wk == detail::kKnobUnset ? 0 : int(wk);
+    key += char(waves);
+    const int64_t pk = detail::knob(detail::kKnobBsPrefetch);
+    const int prefetch = pk == detail::kKnobUnset ? 0 : int(pk);
+    key += char(prefetch);
     JitCache &J = c->jit;
     const bool sync = detail::knob(detail::kKnobBitslice) == 2;
     std::shared_ptr<JitKernel> k;
@@ -137,7 +143,7 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
         }
     }
     if (fresh) {
-        auto src = std::make_shared<std::string>(bs_source(bs_build(coef.data(), int(nd), int(ns), accumulate), gather));
+        auto src = std::make_shared<std::string>(bs_source(bs_build(coef.data(), int(nd), int(ns), accumulate), gather, waves, prefetch));
         const int device = c->device;
         auto done = [&J, k] {
             std::lock_guard<std::mutex> g(J.mu);

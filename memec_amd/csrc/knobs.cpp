@@ -27,6 +27,8 @@ constexpr KnobSpec kSpecs[] = {
     {"MEC_WIDE", kKnobWide, 0, 1, {}, 0},
     {"MEC_MG_ROWS", kKnobMgRows, 3, 8, {3, 4, 8}, 3},
     {"MEC_BITSLICE", kKnobBitslice, 0, 2, {}, 0},
+    {"MEC_BS_WAVES", kKnobBsWaves, 0, 8, {}, 0},
+    {"MEC_BS_PREFETCH", kKnobBsPrefetch, 0, 31, {}, 0},
 };
 // every knob but MEC_SGROUP's run half has its own variable
 static_assert(sizeof(kSpecs) / sizeof(kSpecs[0]) == kKnobCount - 1, "a knob whose variable is never read");

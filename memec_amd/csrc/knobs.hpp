@@ -33,6 +33,8 @@ enum Knob : int {
     kKnobWide,        // MEC_WIDE=0: > 4 outputs as 4-row launches (A/B of gf8_mg_kernel)
     kKnobMgRows,      // MEC_MG_ROWS=3|4|8: rows per group of gf8_mg_kernel
     kKnobBitslice,    // MEC_BITSLICE=0|1|2: wide codes' run-time compiled kernels off / async (default) / sync
+    kKnobBsWaves,     // MEC_BS_WAVES=<n>: those kernels compiled for at least n waves per SIMD (0 = compiler's choice)
+    kKnobBsPrefetch,  // MEC_BS_PREFETCH=<n>: ... with at most n sources' loads ahead of the combine (0 = all first)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

@@ -35,6 +35,9 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
 
 
 ARMS = {"bs": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
+        "bs3": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "3"}, "bs4": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "4"},
+        "bs5": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "5"}, "bsp4": {"MEC_BITSLICE": "2", "MEC_BS_PREFETCH": "4"},
+        "bs4p4": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "4", "MEC_BS_PREFETCH": "4"},
         "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"}}
 
 
@@ -72,7 +75,7 @@ def run(arms_list, steps, warmup, shapes):
             result = lambda: st[:, erased]  # noqa: E731
         arms = {}
         for arm in arms_list:
-            for kn in ("MEC_BITSLICE", "MEC_WIDE"):
+            for kn in ("MEC_BITSLICE", "MEC_WIDE", "MEC_BS_WAVES", "MEC_BS_PREFETCH"):
                 memec_amd.set_knob(kn, ARMS[arm].get(kn))
             for _ in range(warmup):
                 step()
@@ -86,7 +89,7 @@ def run(arms_list, steps, warmup, shapes):
             arms[arm] = {"ms_per_step": round(ms, 4), "GBps": round(alg / (ms * 1e-3) / 1e9, 1),
                          "frac": round(alg / (ms * 1e-3) / 8e12, 4)}
             arms[arm]["digest"] = int(result().view(torch.int64).sum().item())
-        for kn in ("MEC_BITSLICE", "MEC_WIDE"):
+        for kn in ("MEC_BITSLICE", "MEC_WIDE", "MEC_BS_WAVES", "MEC_BS_PREFETCH"):
             memec_amd.set_knob(kn, None)
         rec = {"family": fam, "k": k, "m": m, "chunk": cs, "stripes": n, "op": op, "alg_bytes": alg, **arms}
         if op == "decode":
@@ -122,9 +125,12 @@ if __name__ == "__main__":
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (default: all)")
+    ap.add_argument("--bytewise", action="store_true", help="skip the bitmatrix (Jerasure Cauchy) shapes")
     ap.add_argument("--summarise", nargs=2, metavar=("FETCH_CSV", "WRITE_CSV"))
     a = ap.parse_args()
     shapes = SHAPES if a.shape < 0 else [SHAPES[a.shape]]
+    if a.bytewise:
+        shapes = [x for x in shapes if x[0] != "cauchy"]
     if a.summarise:
         fam, k, m, cs, n, op = shapes[0]
         fk, nf = summarise(a.summarise[0], "FETCH_SIZE", a.steps, a.warmup)
