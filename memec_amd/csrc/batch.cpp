@@ -553,7 +553,7 @@ int run_zerocopy(mec_ctx *c, std::vector<Group> &gs) {
     // no launch may outlive the call (the caller owns the chunks)
     hipError_t e = lane_sync(h.l->stream);
     if (rc == MEC_OK && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
-    if (rc == MEC_OK) c->zc_calls++;
+    if (rc == MEC_OK) count_zc(c);
     return rc;
 }
 
@@ -562,7 +562,7 @@ int run_host(mec_ctx *c, std::vector<Group> &gs) {
         const int zrc = run_zerocopy(c, gs);
         if (zrc != kNotZeroCopy) return zrc;
     }
-    c->staged_calls++;
+    count_staged(c);
     HostPipe &P = c->pipe;
     std::lock_guard<std::mutex> lk(P.mu);
     const size_t cs = c->cs;
@@ -969,9 +969,13 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
     std::lock_guard<std::mutex> lk(c->coal.mu);
     out->coalesced_batches = c->coal.batches;
     out->coalesced_requests = c->coal.requests;
-    out->zero_copy_calls = c->zc_calls.load();
-    out->staged_calls = c->staged_calls.load();
-    out->queue_calls = c->hq ? c->hq->calls.load() : 0;
+    out->zero_copy_calls = out->staged_calls = out->queue_calls = 0;
+    for (const auto &k : c->calls) {
+        out->zero_copy_calls += k.zc.load(std::memory_order_relaxed);
+        out->staged_calls += k.staged.load(std::memory_order_relaxed);
+    }
+    if (c->hq)
+        for (uint32_t i = 0; i < c->hq->slots; ++i) out->queue_calls += c->hq->hs[i].calls.load(std::memory_order_relaxed);
     out->queue_launches = c->hq ? c->hq->launches.load() : 0;
     out->queue_slots = c->hq ? c->hq->slots : 0;
     out->queue_parts = c->hq ? c->hq->parts : 0;

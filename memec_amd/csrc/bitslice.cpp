@@ -195,7 +195,7 @@ struct BsParams {
     i64 sss, dss;
     const u64 *stab, *dtab;
     u32 sstride, dstride;
-    u32 chunk, tiles, nstr, win, s0, pad;
+    u32 chunk, tiles, nstr, win, s0, tpb;
     i64 src_off[32];
     i64 dst_off[32];
 };
@@ -218,9 +218,10 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
         const u32 per = gridDim.x / p.win;
         if (bid < per * p.win) bid = (bid % p.win) * per + bid / p.win;
     }
-    const u32 stripe = bid / p.tiles, tile = bid - stripe * p.tiles;
-    const u32 off = tile * 2048u + threadIdx.x * 16u;
-    if (off >= p.chunk) return;
+    // block b of a stripe codes tiles [b * tpb, (b + 1) * tpb): its chunk
+    // addresses (pointer-row loads when gathered) are read once
+    const u32 stripe = bid / p.tiles, tile0 = (bid - stripe * p.tiles) * p.tpb;
+    if (tile0 * 2048u >= p.chunk) return;
     const u64 gs = (u64)p.s0 + stripe;
 #if MEC_GATHER
     auto src_at = [&](int j) -> u64 { return mec_uniform64(p.stab[gs * p.sstride + p.src_off[j]]); };
@@ -235,21 +236,42 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
     // further source's loads just before the combine of the source `depth`
     // places earlier (depth 0: all loads first)
     const int depth = prefetch > 0 && prefetch < p.ns ? prefetch : p.ns;
+    // chunk addresses at each load / store (24 buffer resources held at
+    // once would be 96 SGPRs and spill into VGPR lanes)
     auto emit_load = [&](int j) {
         std::snprintf(buf, sizeof buf,
-                      "    const __amdgpu_buffer_rsrc_t rs%d = mec_rsrc(src_at(%d), p.chunk);\n"
-                      "    const u32x4 sa%d = LD(rs%d, off), sb%d = LD(rs%d, off + 1024u);\n",
-                      j, j, j, j, j, j);
+                      "    const u32x4 sa%d = LD(mec_rsrc(sp%d, p.chunk), off), sb%d = LD(mec_rsrc(sp%d, p.chunk), off + 1024u);\n",
+                      j, j, j, j);
         s += buf;
     };
+    // (gathered: the pointer-row entry is re-read per tile, from the scalar
+    // cache after the block's first tile; holding all K + R pointers across
+    // the tile loop spilled SGPRs)
+    for (int j = 0; j < p.ns; ++j) {
+        std::snprintf(buf, sizeof buf, "#define sp%d src_at(%d)\n", j, j);
+        s += buf;
+    }
+    for (int r = 0; r < p.nd; ++r) {
+        std::snprintf(buf, sizeof buf, "#define dp%d dst_at(%d)\n", r, r);
+        s += buf;
+    }
+    // gathered kernels loop over the block's tiles; strided ones take one
+    // tile per block (straight-line: the loop costs registers)
+    if (gather)
+        s += "    for (u32 t = 0; t < p.tpb; ++t) {\n"
+             "    const u32 off = (tile0 + t) * 2048u + threadIdx.x * 16u;\n"
+             "    if (off >= p.chunk) break;\n";
+    else
+        s += "    {\n"
+             "    const u32 off = tile0 * 2048u + threadIdx.x * 16u;\n"
+             "    if (off >= p.chunk) return;\n";
     for (int j = 0; j < depth; ++j) emit_load(j);
     int next_load = depth;
     for (int r = 0; r < p.nd; ++r) {
-        std::snprintf(buf, sizeof buf, "    const __amdgpu_buffer_rsrc_t rd%d = mec_rsrc(dst_at(%d), p.chunk);\n", r, r);
-        s += buf;
         if (p.accumulate) {
-            std::snprintf(buf, sizeof buf, "    const u32x4 oa%d = LD(rd%d, off), ob%d = LD(rd%d, off + 1024u);\n", r, r, r,
-                          r);
+            std::snprintf(buf, sizeof buf,
+                          "    const u32x4 oa%d = LD(mec_rsrc(dp%d, p.chunk), off), ob%d = LD(mec_rsrc(dp%d, p.chunk), off + 1024u);\n",
+                          r, r, r, r);
             s += buf;
         }
     }
@@ -290,8 +312,8 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
                 if (all) {
                     const std::vector<int> &w = stored[size_t(o.b)];
                     std::snprintf(buf, sizeof buf,
-                                  "    mec_st(v%d, v%d, v%d, v%d, rd%d, off);\n"
-                                  "    mec_st(v%d, v%d, v%d, v%d, rd%d, off + 1024u);\n",
+                                  "    mec_st(v%d, v%d, v%d, v%d, mec_rsrc(dp%d, p.chunk), off);\n"
+                                  "    mec_st(v%d, v%d, v%d, v%d, mec_rsrc(dp%d, p.chunk), off + 1024u);\n",
                                   w[0], w[1], w[2], w[3], o.b, w[4], w[5], w[6], w[7], o.b);
                 }
                 break;
@@ -299,7 +321,7 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
         }
         s += buf;
     }
-    s += "}\n";
+    s += "    }\n}\n";
     return s;
 }
 

@@ -81,7 +81,7 @@ struct BsParams {
     int64_t sss, dss;
     const uint64_t *stab, *dtab;
     uint32_t sstride, dstride;
-    uint32_t chunk, tiles, nstr, win, s0, pad;
+    uint32_t chunk, tiles, nstr, win, s0, tpb;  // tiles = blocks per stripe, each tpb 2 KiB tiles
     int64_t src_off[32];
     int64_t dst_off[32];
 };

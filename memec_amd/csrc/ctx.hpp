@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -197,7 +198,14 @@ enum : uint32_t { kQCtlStop = 0, kQCtlExit = 1, kQCtlWords = 2 };
 struct HostQueue {
     QSlot *host = nullptr, *dev = nullptr;
     QDevSlot *dslot = nullptr;        // device-memory slot halves (large-BAR devices), else null
-    uint64_t *seqno = nullptr;        // per slot: number of the last job posted (host only)
+    // per slot, host side, on its own cache line (16 server workers posting
+    // at ~1 M calls/s would otherwise bounce one line of flags)
+    struct alignas(64) HostSlotState {
+        std::atomic<bool> busy{false};
+        uint64_t seqno = 0;  // number of the last job posted
+        std::atomic<uint64_t> calls{0};
+    };
+    HostSlotState *hs = nullptr;
     uint32_t *ctl_host = nullptr, *ctl_dev = nullptr;  // [kQCtlStop] host -> GPU, [kQCtlExit] leader -> grid
     uint64_t *act = nullptr;          // device memory: per-slot time of the last job (s_memrealtime)
     // device memory, per slot: [0, slots) the job part 0 took (`go`, read by
@@ -211,11 +219,10 @@ struct HostQueue {
     std::atomic<uint32_t> inflight{0};
     std::atomic<bool> broken{false};  // a call timed out: the queue is stopped for good
     uint64_t idle_ticks = 0, timeout_ms = 5000;
-    std::atomic<bool> *busy = nullptr;
     std::atomic<bool> trace{false};   // mec_queue_trace_enable
     hipStream_t stream = nullptr;
     std::mutex mu;  // launches
-    std::atomic<uint64_t> calls{0}, launches{0};
+    std::atomic<uint64_t> launches{0};
 };
 
 }  // namespace core
@@ -249,7 +256,12 @@ struct mec_ctx {
     mec::core::TableSlot tabs[mec::core::kTableSlots];
     mec::core::HostPipe pipe;
     mec::core::Coalescer coal;
-    std::atomic<uint64_t> zc_calls{0}, staged_calls{0};  // host-call statistics
+    // host-call statistics, striped over cache lines by calling thread
+    struct alignas(64) CallCounters {
+        std::atomic<uint64_t> zc{0}, staged{0};
+    };
+    static constexpr int kCounterStripes = 16;
+    CallCounters calls[kCounterStripes];
     std::mutex hq_mu;
     mec::core::HostQueue *hq = nullptr;  // mec_set_host_queue
     // multi-GPU context (multi.cpp): one ordinary context per device
@@ -281,6 +293,14 @@ namespace mec {
 namespace core {
 
 inline bool has_device(const mec_ctx *c) { return c->device >= 0; }
+
+// The calling thread's stripe of the per-call counters.
+inline mec_ctx::CallCounters &call_counters(mec_ctx *c) {
+    static thread_local const int stripe = int(std::hash<std::thread::id>()(std::this_thread::get_id()) % mec_ctx::kCounterStripes);
+    return c->calls[stripe];
+}
+inline void count_zc(mec_ctx *c) { call_counters(c).zc.fetch_add(1, std::memory_order_relaxed); }
+inline void count_staged(mec_ctx *c) { call_counters(c).staged.fetch_add(1, std::memory_order_relaxed); }
 
 #define CHECK_CTX(c)                                                          \
     do {                                                                      \

@@ -17,8 +17,9 @@
 // pinned, GPU-mapped staging and code there (still no HBM round trip).
 // Registration is Portable: on ROCm the locked range has one device address
 // valid on every GPU, so a multi-device context shares this registry.
-#include <map>
-#include <shared_mutex>
+#include <algorithm>
+#include <atomic>
+#include <mutex>
 
 #include "ctx.hpp"
 
@@ -27,38 +28,61 @@ namespace core {
 namespace {
 
 struct Range {
-    uintptr_t end;
-    uintptr_t dev;
+    uintptr_t begin, end, dev;
 };
 
-std::shared_mutex reg_mu;
-std::map<uintptr_t, Range> reg;  // begin -> range
+// The registry as an immutable snapshot (ranges sorted by begin), replaced
+// as a whole by mec_host_register / mec_host_unregister under reg_mu and
+// read without a lock: every zero-copy host call looks up each of its
+// chunks here, and 16 server workers taking a reader lock per chunk
+// bounced one cache line ~10^7 times a second.  A replaced snapshot is
+// retired, not freed, since a concurrent reader may still hold it; the
+// retired ones are as many as the registration calls (servers register
+// their chunk slabs once).
+struct Snapshot {
+    std::vector<Range> r;
+};
+std::mutex reg_mu;
+std::atomic<const Snapshot *> reg_snap{nullptr};
+std::vector<const Snapshot *> &retired() {
+    static std::vector<const Snapshot *> *v = new std::vector<const Snapshot *>;
+    return *v;
+}
+
+// Caller holds reg_mu: publish `r` as the new snapshot.
+void publish(std::vector<Range> r) {
+    std::sort(r.begin(), r.end(), [](const Range &a, const Range &b) { return a.begin < b.begin; });
+    const Snapshot *n = r.empty() ? nullptr : new Snapshot{std::move(r)};
+    const Snapshot *old = reg_snap.exchange(n, std::memory_order_acq_rel);
+    if (old) retired().push_back(old);
+}
+
+bool lookup(const Snapshot *s, uintptr_t a, size_t len, uint64_t &dev) {
+    const std::vector<Range> &v = s->r;
+    auto it = std::upper_bound(v.begin(), v.end(), a, [](uintptr_t x, const Range &g) { return x < g.begin; });
+    if (it == v.begin()) return false;
+    --it;
+    if (a < it->begin || a + len > it->end) return false;
+    dev = uint64_t(it->dev + (a - it->begin));
+    return true;
+}
 
 }  // namespace
 
 bool zc_device_address(const void *p, size_t len, uint64_t &dev) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    std::shared_lock<std::shared_mutex> lk(reg_mu);
-    if (reg.empty()) return false;
-    auto it = reg.upper_bound(a);
-    if (it == reg.begin()) return false;
-    --it;
-    if (a < it->first || a + len > it->second.end) return false;
-    dev = uint64_t(it->second.dev + (a - it->first));
-    return true;
+    const Snapshot *s = reg_snap.load(std::memory_order_acquire);
+    return s && lookup(s, reinterpret_cast<uintptr_t>(p), len, dev);
 }
 
-bool zc_any_registered() {
-    std::shared_lock<std::shared_mutex> lk(reg_mu);
-    return !reg.empty();
-}
+bool zc_any_registered() { return reg_snap.load(std::memory_order_acquire) != nullptr; }
 
 bool zc_translate(uint64_t *ptrs, size_t n, size_t len) {
-    if (!zc_any_registered()) return false;
+    const Snapshot *s = reg_snap.load(std::memory_order_acquire);
+    if (!s) return false;
     for (size_t i = 0; i < n; ++i) {
         if (!ptrs[i]) continue;  // NULL = zero source / unwanted output
         uint64_t d;
-        if (!zc_device_address(reinterpret_cast<const void *>(uintptr_t(ptrs[i])), len, d)) return false;
+        if (!lookup(s, uintptr_t(ptrs[i]), len, d)) return false;
         ptrs[i] = d;
     }
     return true;
@@ -80,16 +104,28 @@ int mec_host_register(void *ptr, size_t len) {
         (void)hipHostUnregister(ptr);
         return hip_fail(e, "hipHostGetDevicePointer");
     }
-    std::unique_lock<std::shared_mutex> lk(reg_mu);
+    std::lock_guard<std::mutex> lk(reg_mu);
     const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
-    reg[a] = Range{a + len, reinterpret_cast<uintptr_t>(dev)};
+    const Snapshot *cur = reg_snap.load(std::memory_order_acquire);
+    std::vector<Range> r;
+    if (cur)
+        for (const Range &g : cur->r)
+            if (g.begin != a) r.push_back(g);
+    r.push_back(Range{a, a + len, reinterpret_cast<uintptr_t>(dev)});
+    publish(std::move(r));
     return MEC_OK;
 }
 
 int mec_host_unregister(void *ptr) {
     {
-        std::unique_lock<std::shared_mutex> lk(reg_mu);
-        reg.erase(reinterpret_cast<uintptr_t>(ptr));
+        std::lock_guard<std::mutex> lk(reg_mu);
+        const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+        const Snapshot *cur = reg_snap.load(std::memory_order_acquire);
+        std::vector<Range> r;
+        if (cur)
+            for (const Range &g : cur->r)
+                if (g.begin != a) r.push_back(g);
+        publish(std::move(r));
     }
     HIP_TRY(hipHostUnregister(ptr));
     return MEC_OK;

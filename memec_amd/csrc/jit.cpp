@@ -123,7 +123,9 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     const int waves = wk == detail::kKnobUnset ? 0 : int(wk);
     key += char(waves);
     const int64_t pk = detail::knob(detail::kKnobBsPrefetch);
-    const int prefetch = pk == detail::kKnobUnset ? 0 : int(pk);
+    // gathered kernels loop over 4 tiles per block: 4 sources ahead keeps
+    // them at 142 VGPRs (RS(16,8); 235 with every load first)
+    const int prefetch = pk == detail::kKnobUnset ? (gather ? 4 : 0) : int(pk);
     key += char(prefetch);
     JitCache &J = c->jit;
     const bool sync = detail::knob(detail::kKnobBitslice) == 2;
@@ -187,6 +189,7 @@ int jit_launch(mec_ctx *c, JitKernel *k, const BsLaunch &L, hipStream_t stream) 
         const detail::KernelPlan pl = detail::plan_bs(L, s0);
         if (!pl.ok) return fail(MEC_EINVAL, "bit-sliced launch: %s", pl.why);
         p.tiles = pl.geo.tiles;
+        p.tpb = pl.tpb;
         p.nstr = pl.ns;
         p.win = pl.win;
         p.s0 = s0;

@@ -35,6 +35,7 @@ enum Knob : int {
     kKnobBitslice,    // MEC_BITSLICE=0|1|2: wide codes' run-time compiled kernels off / async (default) / sync
     kKnobBsWaves,     // MEC_BS_WAVES=<n>: those kernels compiled for at least n waves per SIMD (0 = compiler's choice)
     kKnobBsPrefetch,  // MEC_BS_PREFETCH=<n>: ... with at most n sources' loads ahead of the combine (0 = all first)
+    kKnobBsTpb,       // MEC_BS_TPB=<n>: 2 KiB tiles per block of the gathered ones (0 = rule: 4)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

@@ -379,9 +379,16 @@ KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
     if (L.k < 1 || L.rows <= kMaxRows || L.k + L.rows > kMaxSrc) return fail_plan(p, "bit-sliced launches take 5..31 rows"), p;
     if (L.len == 0 || L.len % 16 || L.len > (uint64_t(1) << 32) - 2048) return fail_plan(p, "chunk size"), p;
     p.bt = kWaveBlock;
-    // 2 KiB per block: each lane two 16-byte units 1 KiB apart
+    // 2 KiB tiles (each lane two 16-byte units 1 KiB apart), tpb of them
+    // per block: gathered launches read a stripe's K + R chunk pointers
+    // once per block, so a block walks 4 tiles (VERDICT r04 item 6;
+    // MEC_BS_TPB=<n> overrides, experiments); strided blocks take one.
+    const uint32_t tiles = uint32_t((L.len + 2047) / 2048);
+    const int64_t kt = knob(kKnobBsTpb);
+    p.tpb = !L.stab ? 1u : kt != kKnobUnset && kt > 0 ? uint32_t(kt) : 4u;  // strided kernels: one tile
+    p.tpb = std::min(p.tpb, tiles);
     p.geo.units = uint32_t(L.len / 16);
-    p.geo.tiles = uint32_t((L.len + 2047) / 2048);
+    p.geo.tiles = (tiles + p.tpb - 1) / p.tpb;
     p.geo.max_stripes_per_launch = std::max<uint32_t>(1, uint32_t(((uint64_t(1) << 31) / kWaveBlock) / p.geo.tiles));
     p.ns = sub_stripes(p.geo, L.n_stripes, s0);
     p.grid = uint64_t(p.ns) * p.geo.tiles;
@@ -393,7 +400,7 @@ KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
     // occupancy is the program's VGPRs (~190 for 16 sources x 8 rows); only
     // a forced MEC_WPC caps it
     p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0, 0);
-    common_ok(p, uint64_t(p.geo.tiles) * 2048);
+    common_ok(p, uint64_t(p.geo.tiles) * p.tpb * 2048);
     return p;
 }
 

@@ -371,7 +371,7 @@ int zc_single(mec_ctx *c, const std::vector<const uint8_t *> &srcs, const std::v
     {
         int qrc = MEC_OK;
         if (c->hq && queue_try(c, a.data(), srcs.size(), outs.size(), coef, accumulate, qrc)) {
-            if (qrc == MEC_OK) c->zc_calls++;
+            if (qrc == MEC_OK) count_zc(c);
             return qrc;
         }
     }
@@ -387,7 +387,7 @@ int zc_single(mec_ctx *c, const std::vector<const uint8_t *> &srcs, const std::v
     rc = apply(c, b, 0, so, b, 0, dof, coef, 1, accumulate, h.l->stream);
     if (rc != MEC_OK) return rc;
     HIP_TRY(lane_sync(h.l->stream));
-    c->zc_calls++;
+    count_zc(c);
     return MEC_OK;
 }
 
@@ -663,7 +663,7 @@ int mec_encode_host(mec_ctx *c, const uint8_t *const *data, uint8_t *const *pari
         int zrc = zc_single(c, zs, zo, encode_rows(c, rows, cols), false, taken);
         if (taken) return zrc;
     }
-    c->staged_calls++;
+    count_staged(c);
     DeviceGuard dg(c->device);
     int rc = MEC_OK;
     LaneHold h{c, lane_acquire(c, rc)};
@@ -705,7 +705,7 @@ int mec_decode_host(mec_ctx *c, uint8_t *const *chunks, uint64_t present_mask) {
         int zrc = zc_single(c, zs, zo, plan->coef, false, taken);
         if (taken) return zrc;
     }
-    c->staged_calls++;
+    count_staged(c);
     DeviceGuard dg(c->device);
     LaneHold h{c, lane_acquire(c, rc)};
     if (!h.l) return rc;
@@ -739,7 +739,7 @@ int mec_encode_update_host(mec_ctx *c, uint32_t data_index, const uint8_t *delta
         int zrc = zc_single(c, {delta}, zo, encode_rows(c, rows, cols), true, taken);
         if (taken) return zrc;
     }
-    c->staged_calls++;
+    count_staged(c);
     DeviceGuard dg(c->device);
     int rc = MEC_OK;
     LaneHold h{c, lane_acquire(c, rc)};
@@ -788,10 +788,10 @@ int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint
                        n_stripes, false, c->bstream[0]);
         if (rc != MEC_OK) return rc;
         HIP_TRY(hipStreamSynchronize(c->bstream[0]));
-        c->zc_calls++;
+        count_zc(c);
         return MEC_OK;
     }
-    c->staged_calls++;
+    count_staged(c);
     const uint32_t sub = uint32_t(std::max<size_t>(1, std::min<size_t>(n_stripes, (size_t(256) << 20) / per)));
     const size_t need = size_t(sub) * per;
     if (c->bbytes < need) {

@@ -508,8 +508,7 @@ bool queue_stop(mec_ctx *c) {
         (void)hipFree(q->link);
         if (q->dslot) (void)hipFree(q->dslot);
     }
-    delete[] q->busy;
-    delete[] q->seqno;
+    delete[] q->hs;
     delete q;
     return true;
 }
@@ -573,7 +572,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     }
     q->host = static_cast<QSlot *>(h);
     q->dev = static_cast<QSlot *>(d);
-    q->seqno = new uint64_t[slots]();
+    q->hs = new HostQueue::HostSlotState[slots];
     // device-memory slot halves when the host can store to device memory
     // (large BAR): uncached, so part 0's polls and descriptor reads never
     // meet a stale L2 line; MEC_QUEUE_DEVSLOT=0 keeps them in host memory
@@ -597,8 +596,6 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     }
     q->ctl_host = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(h) + sizeof(QSlot) * slots);
     q->ctl_dev = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d) + sizeof(QSlot) * slots);
-    q->busy = new std::atomic<bool>[slots];
-    for (uint32_t i = 0; i < slots; ++i) q->busy[i].store(false);
     e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking);
     // the zeroed per-slot words must be in place before the kernel reads
     // them: a hipMemset need not have finished when work on a non-blocking
@@ -613,8 +610,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
         (void)hipFree(q->act);
         (void)hipFree(q->link);
         if (q->dslot) (void)hipFree(q->dslot);
-        delete[] q->busy;
-        delete[] q->seqno;
+        delete[] q->hs;
         return hip_fail(e, "queue stream");
     }
     {
@@ -626,8 +622,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
             (void)hipFree(q->act);
             (void)hipFree(q->link);
             if (q->dslot) (void)hipFree(q->dslot);
-            delete[] q->busy;
-            delete[] q->seqno;
+            delete[] q->hs;
             return rc;
         }
     }
@@ -640,7 +635,10 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     if (!q || q->broken.load(std::memory_order_relaxed) || c->cs > q->max_chunk || ns > kQMaxSrc ||
         nd > kQMaxDst || nd == 0 || (!c->byte_wise() && (c->w < 1 || c->w > 8)))
         return false;
-    if (c->cs > q->solo_max && q->inflight.load(std::memory_order_relaxed) == 0) return false;
+    // the in-flight count only matters to chunks above solo_max (no RMW on a
+    // shared line per call otherwise)
+    const bool track = c->cs > q->solo_max;
+    if (track && q->inflight.load(std::memory_order_relaxed) == 0) return false;
     // a free slot, starting from a per-thread hint so callers spread out
     static thread_local uint32_t hint = uint32_t(std::hash<std::thread::id>()(std::this_thread::get_id()));
     uint32_t i = 0;
@@ -648,11 +646,11 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
     for (uint32_t n = 0; n < q->slots && !got; ++n) {
         i = (hint + n) % q->slots;
         bool f = false;
-        got = !q->busy[i].load(std::memory_order_relaxed) && q->busy[i].compare_exchange_strong(f, true);
+        got = !q->hs[i].busy.load(std::memory_order_relaxed) && q->hs[i].busy.compare_exchange_strong(f, true);
     }
     if (!got) return false;  // every slot busy: the launch path takes this call
     hint = i;
-    q->inflight.fetch_add(1, std::memory_order_relaxed);
+    if (track) q->inflight.fetch_add(1, std::memory_order_relaxed);
     QSlot *s = q->host + i;
     QDesc &d = s->d;  // built in host memory (the device copy follows, below)
     d.hdr[0] = uint32_t(ns);
@@ -674,8 +672,8 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
             for (size_t j = 0; j < ns; ++j) bit_block(f, coef[r * ns + j], c->w, &mk[j][r * c->w], 1);
         std::memcpy(d.mask_w, mk, sizeof(mk));
     }
-    const uint64_t seq = q->seqno[i] + 1;
-    q->seqno[i] = seq;
+    const uint64_t seq = q->hs[i].seqno + 1;
+    q->hs[i].seqno = seq;
     const uint64_t t_post = traced ? mono_ns() : 0;
     // publishes the descriptor; the word carries its shape (sources, outputs)
     const uint64_t word = seq << 16 | uint64_t(ns) << 8 | uint64_t(nd);
@@ -722,7 +720,7 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
                 // may still be written; an accumulate job must not be run
                 // again on top of the parts that applied it).
                 if (dt > std::chrono::milliseconds(q->timeout_ms)) q->timeouts++;
-                q->seqno[i] = seq - 1;
+                q->hs[i].seqno = seq - 1;
                 if (q->dslot) {
                     _mm_stream_si64(reinterpret_cast<long long *>(&q->dslot[i].seq), static_cast<long long>((seq - 1) << 16));
                     _mm_sfence();
@@ -768,10 +766,10 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
         tr.parts = q->parts;
         tr.valid = 1;
     }
-    q->inflight.fetch_sub(1, std::memory_order_relaxed);
+    if (track) q->inflight.fetch_sub(1, std::memory_order_relaxed);
     if (rc == MEC_OK && taken) {
-        q->busy[i].store(false, std::memory_order_release);
-        q->calls++;
+        q->hs[i].calls.fetch_add(1, std::memory_order_relaxed);
+        q->hs[i].busy.store(false, std::memory_order_release);
     }
     return taken;
 }

@@ -179,10 +179,11 @@ static void check_bs(int k, int rows, uint64_t chunk, uint32_t n, bool in_place,
     uint64_t covered = 0;
     for (uint32_t s0 = 0; s0 < n;) {
         const KernelPlan p = plan_bs(L, s0);
-        common(p, uint64_t(p.geo.tiles) * 2048);
+        common(p, uint64_t(p.geo.tiles) * p.tpb * 2048);
         if (!p.ok || p.ns == 0) break;
         if (p.bt != uint32_t(kWaveBlock)) bad("bit-sliced kernels are one-wave blocks", p);
-        if (uint64_t(p.geo.tiles) * 2048 < chunk) bad("tiles do not cover the chunk", p);
+        if (p.tpb < 1 || uint64_t(p.geo.tiles) * p.tpb * 2048 < chunk) bad("tiles do not cover the chunk", p);
+        if (uint64_t(p.geo.tiles - 1) * p.tpb * 2048 >= chunk) bad("a block with no tile", p);
         covered += p.ns;
         s0 += p.ns;
     }

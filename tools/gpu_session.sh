@@ -78,11 +78,8 @@ for step in "$@"; do
                     SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
                     --output-format csv -d "$OUT/pmc_sqlds_$c" -o run -- python3 bench.py --config "$c" --no-cpu-baseline --no-extra-configs --no-ceiling --steps 3 --warmup 1
             done ;;
-        wide) run wide_ab 600 python tools/wide_ab.py --steps 10 ;;
+        wide) run wide_ab 600 python tools/wide_ab.py --bytewise --arms bs,mg --steps 10 ;;
         server) run server_pattern 900 bash tools/server_pattern.sh ;;
-        stagger) run stagger_probe 300 tools/stagger_probe 4096 3 ;;
-        wider8) run wide_r8_probe 300 tools/wide_r8_probe 16384 3 ;;
-        bar) run bar_probe 120 tools/bar_probe 2000 ;;
         tsan)  # host-TSan build (tools/tsan_build.sh, built beforehand): concurrent callers
             export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 exitcode=0 suppressions=$PWD/tools/tsan_suppressions.txt"
             for c in rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536; do
@@ -109,22 +106,9 @@ for step in "$@"; do
             run asan_latency_rs 120 tools/queue_latency_asan rs 8 2 4096 3000 1 1
             run asan_latency_cauchy 120 tools/queue_latency_asan cauchy 4 2 4096 3000 0 2
             grep -l "ERROR: AddressSanitizer" "$OUT"/asan_*.log > "$OUT/asan_errors.txt" || true ;;
-        staggerpmc)  # EA counters per stagger_probe arm (tools/stagger_pmc.py)
-            arms=${STAGGER_ARMS:-split_enc,split_twin_cap12,split_dense_cap12,inplace_dec,inplace_dec_sleep32,inplace_twin,inplace_vand}
-            run stagger_plain 200 tools/stagger_probe 2048 1 "$arms"
-            run stagger_pmc_a 200 timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_LEVEL_sum \
-                TCC_EA0_WRREQ_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/stagger_pmc_a" -o run -- tools/stagger_probe 2048 1 "$arms"
-            run stagger_pmc_b 200 timeout -s KILL 150 rocprofv3 --pmc TCC_EA0_WRREQ_STALL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum \
-                TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum GRBM_GUI_ACTIVE --output-format csv -d "$OUT/stagger_pmc_b" -o run -- tools/stagger_probe 2048 1 "$arms"
-            run stagger_pmc_c 200 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU \
-                SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/stagger_pmc_c" -o run -- tools/stagger_probe 2048 1 "$arms"
-            python3 tools/stagger_pmc.py "$arms" "$OUT/stagger_pmc_a" "$OUT/stagger_pmc_b" "$OUT/stagger_pmc_c" > "$OUT/stagger_pmc.jsonl" ;;
-        mixed)
-            for w in 1 4 16; do
-                run "mixed_w$w" 120 tools/mixed_ab 1024 $w 3 32
-            done
-            grep -h '^{' "$OUT"/mixed_w*.log > "$OUT/mixed.jsonl" ;;
-        latency)
+        latency)  # single-caller queue latency, traced (tools/queue_latency.hip, built here)
+            /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 -std=c++17 -Iinclude tools/queue_latency.hip -Lmemec_amd -lmec \
+                -Wl,-rpath,"$PWD/memec_amd" -o tools/queue_latency || exit 1
             for env in ${LAT_ENVS:-MEC_QUEUE_TIMEOUT_MS=5000}; do  # ','-separated settings per run
                 for a in ${LAT_ARGS:-rs,8,2,4096,20000,1,1 rs,8,2,4096,20000,0,1 rs,4,2,4096,20000,1,1 \
                          rs,10,4,65536,5000,1,1 cauchy,4,2,4096,20000,1,1 rs,8,2,4096,20000,1,2}; do
@@ -135,12 +119,12 @@ for step in "$@"; do
                     sed "s/^{/{\"env\": \"$env\", /" "$OUT/latency_$tag.log" | grep '^{' >> "$OUT/latency.jsonl"
                 done
             done ;;
-        widepmc)
+        widepmc)  # HBM traffic of one wide shape per kernel arm (WIDE_SHAPES, WIDE_ARMS)
             for sh in ${WIDE_SHAPES:-0 1}; do
-                for mode in wide split; do
+                for arm in ${WIDE_ARMS:-bs mg}; do
                     for ctr in FETCH_SIZE WRITE_SIZE; do
-                        run "pmc_wide_${sh}_${mode}_${ctr}" 300 rocprofv3 --pmc $ctr --output-format csv \
-                            -d "$OUT/pmc_wide_${sh}_${mode}_${ctr}" -o run -- python3 tools/wide_ab.py --mode $mode --shape $sh --steps 5 --warmup 1
+                        run "pmc_wide_${sh}_${arm}_${ctr}" 300 rocprofv3 --pmc $ctr --output-format csv \
+                            -d "$OUT/pmc_wide_${sh}_${arm}_${ctr}" -o run -- python3 tools/wide_ab.py --arms $arm --shape $sh --steps 5 --warmup 1
                     done
                 done
             done ;;

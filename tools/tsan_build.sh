@@ -29,7 +29,7 @@ for f in memec_amd/csrc/*.hip memec_amd/csrc/*.cpp; do
     fi
 done
 for p in "${pids[@]}"; do wait "$p"; done
-$HIPCC --offload-arch=gfx950 -shared -fPIC -o "$LIB/libmec.so" "${objs[@]}" -Wl,-soname,libmec.so
+$HIPCC --offload-arch=gfx950 -shared -fPIC -o "$LIB/libmec.so" "${objs[@]}" -Wl,-soname,libmec.so -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 $CLANG -std=c++11 -O1 -g -fsanitize=thread -fno-omit-frame-pointer -Imemec_amd/csrc/coding -Iinclude \
     tools/coding_bench.cc memec_amd/csrc/coding/*.cc -L"$LIB" -lmec -Wl,-rpath,'$ORIGIN/../memec_amd/tsan' \
     -lpthread -o tools/coding_bench_tsan

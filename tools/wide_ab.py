@@ -31,13 +31,17 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("cauchy", 20, 8, 40960, 8192, "encode"), ("cauchy", 20, 8, 40960, 8192, "decode"),
           ("rs", 16, 8, 65536, 16384, "batch"), ("isal_rs", 12, 8, 65536, 16384, "batch"),
           ("cauchy", 10, 6, 65536, 16384, "batch"), ("rs", 10, 4, 1 << 20, 4096, "batch"),
-          ("rs", 10, 4, 1 << 20, 4096, "encode")]
+          ("rs", 10, 4, 1 << 20, 4096, "encode"), ("rs", 4, 12, 1 << 20, 512, "decode"),
+          ("isal_cauchy", 4, 12, 1 << 20, 512, "encode"), ("rs", 10, 6, 262144, 4096, "batch"),
+          ("rs", 16, 8, 65536, 16384, "batchdec")]
 
 
 ARMS = {"bs": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
         "bs3": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "3"}, "bs4": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "4"},
         "bs5": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "5"}, "bsp4": {"MEC_BITSLICE": "2", "MEC_BS_PREFETCH": "4"},
         "bs4p4": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "4", "MEC_BS_PREFETCH": "4"},
+        "bst1": {"MEC_BITSLICE": "2", "MEC_BS_TPB": "1"}, "bst2": {"MEC_BITSLICE": "2", "MEC_BS_TPB": "2"},
+        "bst8": {"MEC_BITSLICE": "2", "MEC_BS_TPB": "8"}, "bst16": {"MEC_BITSLICE": "2", "MEC_BS_TPB": "16"},
         "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"}}
 
 
@@ -56,9 +60,11 @@ def run(arms_list, steps, warmup, shapes):
             if op == "encode":
                 step = lambda: c.encode(data, par)  # noqa: E731
             else:  # the pointer-array ABI (mec_encode_batch) over the same chunks
+                # uint64 arrays built once (no per-step Python list conversion)
+                import numpy as np
                 db, pb = data.data_ptr(), par.data_ptr()
-                dptr = [db + (s * k + j) * cs for s in range(n) for j in range(k)]
-                pptr = [pb + (s * m + i) * cs for s in range(n) for i in range(m)]
+                dptr = (db + (np.arange(n, dtype=np.uint64)[:, None] * k + np.arange(k, dtype=np.uint64)) * cs).ravel()
+                pptr = (pb + (np.arange(n, dtype=np.uint64)[:, None] * m + np.arange(m, dtype=np.uint64)) * cs).ravel()
                 step = lambda: c.encode_batch(dptr, pptr, mem="device")  # noqa: E731
             alg = (k + m) * cs * n
             result = lambda: par  # noqa: E731
@@ -70,12 +76,19 @@ def run(arms_list, steps, warmup, shapes):
             present = sum(1 << i for i in range(k + m) if i not in erased)
             orig = st[:, erased].clone()
             st[:, erased] = 0
-            step = lambda: c.decode(st, present)  # noqa: E731
+            if op == "batchdec":  # the pointer-array ABI (mec_decode_batch), one pattern: one-map batch
+                import numpy as np
+                sb = st.data_ptr()
+                cptr = (sb + (np.arange(n, dtype=np.uint64)[:, None] * (k + m) + np.arange(k + m, dtype=np.uint64)) * cs).ravel()
+                masks = np.full(n, present, dtype=np.uint64)
+                step = lambda: c.decode_batch(cptr, masks, mem="device")  # noqa: E731
+            else:
+                step = lambda: c.decode(st, present)  # noqa: E731
             alg = (k + m) * cs * n
             result = lambda: st[:, erased]  # noqa: E731
         arms = {}
         for arm in arms_list:
-            for kn in ("MEC_BITSLICE", "MEC_WIDE", "MEC_BS_WAVES", "MEC_BS_PREFETCH"):
+            for kn in ("MEC_BITSLICE", "MEC_WIDE", "MEC_BS_WAVES", "MEC_BS_PREFETCH", "MEC_BS_TPB"):
                 memec_amd.set_knob(kn, ARMS[arm].get(kn))
             for _ in range(warmup):
                 step()
@@ -89,7 +102,7 @@ def run(arms_list, steps, warmup, shapes):
             arms[arm] = {"ms_per_step": round(ms, 4), "GBps": round(alg / (ms * 1e-3) / 1e9, 1),
                          "frac": round(alg / (ms * 1e-3) / 8e12, 4)}
             arms[arm]["digest"] = int(result().view(torch.int64).sum().item())
-        for kn in ("MEC_BITSLICE", "MEC_WIDE", "MEC_BS_WAVES", "MEC_BS_PREFETCH"):
+        for kn in ("MEC_BITSLICE", "MEC_WIDE", "MEC_BS_WAVES", "MEC_BS_PREFETCH", "MEC_BS_TPB"):
             memec_amd.set_knob(kn, None)
         rec = {"family": fam, "k": k, "m": m, "chunk": cs, "stripes": n, "op": op, "alg_bytes": alg, **arms}
         if op == "decode":
@@ -126,11 +139,14 @@ if __name__ == "__main__":
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (default: all)")
     ap.add_argument("--bytewise", action="store_true", help="skip the bitmatrix (Jerasure Cauchy) shapes")
+    ap.add_argument("--ops", default="", help="comma-separated ops to keep (encode, decode, batch)")
     ap.add_argument("--summarise", nargs=2, metavar=("FETCH_CSV", "WRITE_CSV"))
     a = ap.parse_args()
     shapes = SHAPES if a.shape < 0 else [SHAPES[a.shape]]
     if a.bytewise:
         shapes = [x for x in shapes if x[0] != "cauchy"]
+    if a.ops:
+        shapes = [x for x in shapes if x[5] in a.ops.split(",")]
     if a.summarise:
         fam, k, m, cs, n, op = shapes[0]
         fk, nf = summarise(a.summarise[0], "FETCH_SIZE", a.steps, a.warmup)
