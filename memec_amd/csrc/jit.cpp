@@ -106,9 +106,23 @@ uint64_t env_u64(const char *name, uint64_t dflt) {
 
 }  // namespace
 
-bool jit_wanted(const mec_ctx *c, size_t nd) {
+// Which wide launches take the bit-sliced kernel (MEC_BITSLICE unset, 1 or
+// 2): every dense matrix (decodes, ISA-L Cauchy), and Vandermonde-structured
+// ones (row 0 and column 0 all ones: Jerasure / ISA-L RS encodes) from 12
+// sources up.  There gf8_mg_kernel's plain-XOR row and column are cheap
+// enough that it stays ahead: RS(10,6)@256 KiB encode 74 % against 67-70,
+// RS(4,12)@1 MiB 78 against 61, RS(8,5)@16 KiB even; RS(16,8) 72-74
+// against 65-67, ISA-L RS(12,8) 79 against 66, every dense shape +8-24
+// points (tools/wide_ab.py, profiles/r05/wide_ab_*.jsonl).  MEC_BITSLICE=3
+// takes it for every wide launch (A/B), 0 never.
+bool jit_wanted(const mec_ctx *c, size_t nd, size_t ns, const Mat &coef) {
     const int64_t kn = detail::knob(detail::kKnobBitslice);
-    return kn != 0 && c->byte_wise() && nd > size_t(kMaxRows) && c->cs % 16 == 0;
+    if (kn == 0 || !c->byte_wise() || nd <= size_t(kMaxRows) || c->cs % 16 != 0) return false;
+    if (kn == 3) return true;
+    bool vand = true;
+    for (size_t j = 0; j < ns && vand; ++j) vand = coef[j] == 1;
+    for (size_t r = 0; r < nd && vand; ++r) vand = coef[r * ns] == 1;
+    return !vand || ns >= 12;
 }
 
 // The kernel for (coef, accumulate, addressing), compiling it if needed;
@@ -128,7 +142,7 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     const int prefetch = pk == detail::kKnobUnset ? (gather ? 4 : 0) : int(pk);
     key += char(prefetch);
     JitCache &J = c->jit;
-    const bool sync = detail::knob(detail::kKnobBitslice) == 2;
+    const bool sync = detail::knob(detail::kKnobBitslice) >= 2;
     std::shared_ptr<JitKernel> k;
     bool fresh = false;
     {

@@ -26,7 +26,7 @@ constexpr KnobSpec kSpecs[] = {
     {"MEC_COPY_THREADS", kKnobCopyThreads, 1, 64, {}, 0},
     {"MEC_WIDE", kKnobWide, 0, 1, {}, 0},
     {"MEC_MG_ROWS", kKnobMgRows, 3, 8, {3, 4, 8}, 3},
-    {"MEC_BITSLICE", kKnobBitslice, 0, 2, {}, 0},
+    {"MEC_BITSLICE", kKnobBitslice, 0, 3, {}, 0},
     {"MEC_BS_WAVES", kKnobBsWaves, 0, 8, {}, 0},
     {"MEC_BS_PREFETCH", kKnobBsPrefetch, 0, 31, {}, 0},
     {"MEC_BS_TPB", kKnobBsTpb, 0, 64, {}, 0},

@@ -405,13 +405,13 @@ BS_SHAPES = [(16, 8, 8192, 3), (12, 8, 4096, 3), (10, 6, 2048, 4), (8, 5, 3072, 
 
 @pytest.mark.parametrize("fam", ["rs", "isal_rs", "isal_cauchy"])
 def test_bitslice_encode_decode_update_vs_oracle(fam, knobs):
-    """MEC_BITSLICE=2 (compile at first use): every > 4-output launch runs
-    the matrix's own bit-sliced kernel — encode split and in place, decodes
+    """MEC_BITSLICE=3 (compile at first use, every wide launch): every >
+    4-output launch runs the matrix's own bit-sliced kernel — encode split and in place, decodes
     of 5..m erasures in place and split (random non-codeword stripes pin the
     decoding matrix), accumulating updates — on chunks that are and are not
     multiples of the 2 KiB tile (16, 1040, 2064, 3072 bytes), equal to the
     oracle; the stats show the kernels built and launched, none failed."""
-    knobs("MEC_BITSLICE", "2")
+    knobs("MEC_BITSLICE", "3")
     for k, m, cs, n in BS_SHAPES:
         data = O.fill(n * k * cs, 7000 + k * 10 + m).reshape(n, k, cs)
         want = np.stack([np.stack(O.encode(fam, k, m, [data[s, j].copy() for j in range(k)], cs)) for s in range(n)])
@@ -450,7 +450,33 @@ def test_bitslice_encode_decode_update_vs_oracle(fam, knobs):
         want2 = np.stack([np.stack(O.encode(fam, k, m, [d2[s, jj].copy() for jj in range(k)], cs)) for s in range(n)])
         assert np.array_equal(host(par), want2), (fam, k, m, cs, "update")
         s = c.stats()
-        assert s["jit_failed"] == 0 and s["jit_kernels"] >= 2 and s["jit_launches"] >= 3, s
+        assert s["jit_failed"] == 0 and s["jit_kernels"] >= 4 and s["jit_launches"] >= 6, s
+        c.close()
+
+
+def test_bitslice_rule(knobs):
+    """MEC_BITSLICE=2: the rule (jit.cpp jit_wanted) — Vandermonde-structured
+    encodes under 12 sources stay on gf8_mg_kernel, from 12 up and every
+    dense matrix (a decode) take the bit-sliced kernel; same bytes."""
+    knobs("MEC_BITSLICE", "2")
+    for k, m, cs, want_enc in [(10, 6, 2048, False), (12, 6, 2048, True)]:
+        n = 2
+        data = O.fill(n * k * cs, 9100 + k).reshape(n, k, cs)
+        want = np.stack([np.stack(O.encode("rs", k, m, [data[s, j].copy() for j in range(k)], cs)) for s in range(n)])
+        c = Codec("rs", k, m, cs)
+        par = torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)
+        c.encode(dev(data), par)
+        assert np.array_equal(host(par), want)
+        assert (c.stats()["jit_launches"] == 1) == want_enc, (k, m, c.stats())
+        st = torch.cat([dev(data), par], dim=1)
+        t = st.clone()
+        pat = list(range(m))
+        t[:, pat] = 0
+        before = c.stats()["jit_launches"]
+        c.decode(t, sum(1 << i for i in range(k + m) if i not in pat))
+        torch.cuda.synchronize()
+        assert torch.equal(t, st)
+        assert c.stats()["jit_launches"] == before + 1, c.stats()
         c.close()
 
 
@@ -485,10 +511,12 @@ def test_bitslice_async_takes_over(knobs):
 @pytest.mark.parametrize("mem", ["device", "host"])
 def test_bitslice_pointer_batch_one_map(mem, knobs):
     """Pointer batches with one map and > 4 outputs through the gathered
-    bit-sliced kernel (scattered 8-byte-aligned ChunkPool-like slots, a
-    Coding::zeros column): RS(16,8) and ISA-L Cauchy(10,6) encode, then the
-    same 6 erasures rebuilt in place in every stripe."""
+    bit-sliced kernel (scattered 8-byte-aligned ChunkPool-like slots; its
+    blocks walk 4 tiles, and 1, 3 and 16 here): RS(16,8) and ISA-L
+    Cauchy(10,6) encode, then the same 6 erasures rebuilt in place in every
+    stripe."""
     knobs("MEC_BITSLICE", "2")
+    knobs("MEC_BS_TPB", {"device": "3", "host": None}[mem])
     for fam, k, m, cs, n in [("rs", 16, 8, 4096, 12), ("isal_cauchy", 10, 6, 2064, 10)]:
         rng = np.random.default_rng(k * 7 + m)
         slots = rng.permutation(n * (k + m))

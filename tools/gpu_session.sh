@@ -128,6 +128,17 @@ for step in "$@"; do
                     done
                 done
             done ;;
+        channels)  # per-TCC-instance EA requests of RS(10,4)@1 MiB arms (tools/channel_probe.py), 4 counters a pass
+            for arm in ${CH_ARMS:-enc_split dec_inplace dec_split}; do
+                run "ch_plain_$arm" 120 python3 tools/channel_probe.py $arm 5
+                for kind in RD WR; do
+                    for q in 0 4 8 12; do
+                        ctrs="MEC_EA_${kind}_CH$q MEC_EA_${kind}_CH$((q + 1)) MEC_EA_${kind}_CH$((q + 2)) MEC_EA_${kind}_CH$((q + 3))"
+                        run "ch_${arm}_${kind}_$q" 120 timeout -s KILL 100 rocprofv3 -E tools/ea_channels.yaml --pmc $ctrs \
+                            --output-format csv -d "$OUT/ch_${arm}_${kind}_$q" -o run -- python3 tools/channel_probe.py $arm 3
+                    done
+                done
+            done ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

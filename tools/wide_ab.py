@@ -36,12 +36,12 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("rs", 16, 8, 65536, 16384, "batchdec")]
 
 
-ARMS = {"bs": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
-        "bs3": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "3"}, "bs4": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "4"},
-        "bs5": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "5"}, "bsp4": {"MEC_BITSLICE": "2", "MEC_BS_PREFETCH": "4"},
-        "bs4p4": {"MEC_BITSLICE": "2", "MEC_BS_WAVES": "4", "MEC_BS_PREFETCH": "4"},
-        "bst1": {"MEC_BITSLICE": "2", "MEC_BS_TPB": "1"}, "bst2": {"MEC_BITSLICE": "2", "MEC_BS_TPB": "2"},
-        "bst8": {"MEC_BITSLICE": "2", "MEC_BS_TPB": "8"}, "bst16": {"MEC_BITSLICE": "2", "MEC_BS_TPB": "16"},
+ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
+        "bs3": {"MEC_BITSLICE": "3", "MEC_BS_WAVES": "3"}, "bs4": {"MEC_BITSLICE": "3", "MEC_BS_WAVES": "4"},
+        "bs5": {"MEC_BITSLICE": "3", "MEC_BS_WAVES": "5"}, "bsp4": {"MEC_BITSLICE": "3", "MEC_BS_PREFETCH": "4"},
+        "bs4p4": {"MEC_BITSLICE": "3", "MEC_BS_WAVES": "4", "MEC_BS_PREFETCH": "4"},
+        "bst1": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "1"}, "bst2": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "2"},
+        "bst8": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "8"}, "bst16": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "16"},
         "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"}}
 
 
