@@ -128,6 +128,14 @@ for step in "$@"; do
                     done
                 done
             done ;;
+        widesq)  # VALU issue and occupancy of one wide shape per kernel arm (WIDE_SHAPES, WIDE_ARMS)
+            for sh in ${WIDE_SHAPES:-0}; do
+                for arm in ${WIDE_ARMS:-bs mg}; do
+                    run "pmc_widesq_${sh}_${arm}" 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU \
+                        SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE \
+                        --output-format csv -d "$OUT/pmc_widesq_${sh}_${arm}" -o run -- python3 tools/wide_ab.py --arms $arm --shape $sh --steps 3 --warmup 1
+                done
+            done ;;
         channels)  # per-TCC-instance EA requests of RS(10,4)@1 MiB arms (tools/channel_probe.py), 4 counters a pass
             for arm in ${CH_ARMS:-enc_split dec_inplace dec_split}; do
                 run "ch_plain_$arm" 120 python3 tools/channel_probe.py $arm 5
