@@ -178,7 +178,7 @@ void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out) 
     }
 }
 
-std::string bs_source(const BsProgram &p, bool gather, int waves, int prefetch) {
+std::string bs_source(const BsProgram &p, bool gather, int waves, int prefetch, bool loop) {
     std::string s;
     s.reserve(p.ops.size() * 48 + 4096);
     s += gather ? "#define MEC_GATHER 1\n" : "#define MEC_GATHER 0\n";
@@ -255,9 +255,9 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
         std::snprintf(buf, sizeof buf, "#define dp%d dst_at(%d)\n", r, r);
         s += buf;
     }
-    // gathered kernels loop over the block's tiles; strided ones take one
+    // looped gathered kernels walk the block's tiles; the others take one
     // tile per block (straight-line: the loop costs registers)
-    if (gather)
+    if (gather && loop)
         s += "    for (u32 t = 0; t < p.tpb; ++t) {\n"
              "    const u32 off = (tile0 + t) * 2048u + threadIdx.x * 16u;\n"
              "    if (off >= p.chunk) break;\n";

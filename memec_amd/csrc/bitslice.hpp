@@ -69,7 +69,9 @@ void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out);
 // (amdgpu_waves_per_eu; the register budget shrinks accordingly).
 // prefetch > 0: at most that many sources' loads issued ahead of the
 // combine (0: every load first).
-std::string bs_source(const BsProgram &p, bool gather, int waves = 0, int prefetch = 0);
+// loop (gathered only): the block walks p.tpb tiles per pointer-row read;
+// otherwise it codes one tile, straight-line (launch with tpb = 1).
+std::string bs_source(const BsProgram &p, bool gather, int waves = 0, int prefetch = 0, bool loop = false);
 
 // Kernel arguments of every generated kernel (the same layout in the
 // generated source, bs_source).  Strided: source j of stripe s at src + s *

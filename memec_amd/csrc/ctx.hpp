@@ -181,6 +181,7 @@ struct JitKernel {
     hipFunction_t fn = nullptr;
     double compile_ms = 0;
     std::string err;
+    uint32_t tpb = 1;  // gathered: tiles per block it was built for (> 1: looped)
 };
 struct JitCache {
     std::mutex mu;

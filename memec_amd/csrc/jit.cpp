@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <deque>
 #include <thread>
 
@@ -107,18 +108,22 @@ uint64_t env_u64(const char *name, uint64_t dflt) {
 }  // namespace
 
 // Which wide launches take the bit-sliced kernel (MEC_BITSLICE unset, 1 or
-// 2): every dense matrix (decodes, ISA-L Cauchy), and Vandermonde-structured
-// ones (row 0 and column 0 all ones: Jerasure / ISA-L RS encodes) from 12
-// sources up.  There gf8_mg_kernel's plain-XOR row and column are cheap
-// enough that it stays ahead: RS(10,6)@256 KiB encode 74 % against 67-70,
-// RS(4,12)@1 MiB 78 against 61, RS(8,5)@16 KiB even; RS(16,8) 72-74
-// against 65-67, ISA-L RS(12,8) 79 against 66, every dense shape +8-24
-// points (tools/wide_ab.py, profiles/r05/wide_ab_*.jsonl).  MEC_BITSLICE=3
-// takes it for every wide launch (A/B), 0 never.
+// 2): matrices with at least half as many sources as outputs that are
+// dense (decodes, ISA-L Cauchy) or have 12+ sources.  Below 12 sources a
+// Vandermonde-structured matrix (row 0 and column 0 all ones: Jerasure /
+// ISA-L RS encodes) keeps gf8_mg_kernel, whose plain-XOR row and column make
+// it cheaper there: RS(10,6)@256 KiB encode 74-75 % against 67-72, RS(8,5)
+// @16 KiB even; with fewer than half as many sources as outputs the
+// bit-sliced kernel's per-output work dominates: RS(4,12)@1 MiB encode 61
+// against 78, ISA-L Cauchy(4,12) 62 against 76.  RS(16,8) 71-74 against
+// 64-67, ISA-L RS(12,8) 79 against 65, the other dense shapes +8-24 points
+// (tools/wide_ab.py, profiles/r05/wide_ab_*.jsonl).  MEC_BITSLICE=3 takes
+// it for every wide launch (A/B), 0 never.
 bool jit_wanted(const mec_ctx *c, size_t nd, size_t ns, const Mat &coef) {
     const int64_t kn = detail::knob(detail::kKnobBitslice);
     if (kn == 0 || !c->byte_wise() || nd <= size_t(kMaxRows) || c->cs % 16 != 0) return false;
     if (kn == 3) return true;
+    if (nd > 2 * ns) return false;
     bool vand = true;
     for (size_t j = 0; j < ns && vand; ++j) vand = coef[j] == 1;
     for (size_t r = 0; r < nd && vand; ++r) vand = coef[r * ns] == 1;
@@ -136,10 +141,17 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     const int64_t wk = detail::knob(detail::kKnobBsWaves);  // experiments (mec_set_knob)
     const int waves = wk == detail::kKnobUnset ? 0 : int(wk);
     key += char(waves);
+    // gathered: one straight-line tile per block (the strided kernel's
+    // shape), unless MEC_BS_TPB asks for a loop over several tiles per
+    // pointer-row read.  Every form keeps 4 sources' loads ahead of the
+    // combine: RS(16,8) strided 141 VGPRs (163 with every load first),
+    // gathered 156 (207), looped 165 (235) — 3 waves per SIMD, no scratch
+    // (test_abi.py::test_bitslice_kernels_compile_for_gfx950).
+    const uint32_t tpb = gather ? std::min<uint32_t>(detail::bs_gather_tpb(), 255u) : 1u;
+    const bool loop = tpb > 1;
+    key += char(tpb);
     const int64_t pk = detail::knob(detail::kKnobBsPrefetch);
-    // gathered kernels loop over 4 tiles per block: 4 sources ahead keeps
-    // them at 142 VGPRs (RS(16,8); 235 with every load first)
-    const int prefetch = pk == detail::kKnobUnset ? (gather ? 4 : 0) : int(pk);
+    const int prefetch = pk == detail::kKnobUnset ? 4 : int(pk);
     key += char(prefetch);
     JitCache &J = c->jit;
     const bool sync = detail::knob(detail::kKnobBitslice) >= 2;
@@ -153,13 +165,14 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
         } else {
             if (J.map.size() >= J.cap) return nullptr;
             k = std::make_shared<JitKernel>();
+            k->tpb = tpb;
             J.map.emplace(key, k);
             fresh = true;
             ++J.pending;
         }
     }
     if (fresh) {
-        auto src = std::make_shared<std::string>(bs_source(bs_build(coef.data(), int(nd), int(ns), accumulate), gather, waves, prefetch));
+        auto src = std::make_shared<std::string>(bs_source(bs_build(coef.data(), int(nd), int(ns), accumulate), gather, waves, prefetch, loop));
         const int device = c->device;
         auto done = [&J, k] {
             std::lock_guard<std::mutex> g(J.mu);
@@ -186,7 +199,9 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     return k->state.load(std::memory_order_acquire) > 0 ? k.get() : nullptr;
 }
 
-int jit_launch(mec_ctx *c, JitKernel *k, const BsLaunch &L, hipStream_t stream) {
+int jit_launch(mec_ctx *c, JitKernel *k, const BsLaunch &L0, hipStream_t stream) {
+    BsLaunch L = L0;
+    L.tpb = L.stab ? k->tpb : 1u;  // the tiles per block this kernel was built for
     BsParams p{};
     p.src = L.src;
     p.dst = L.dst;

@@ -163,6 +163,7 @@ struct BsLaunch {
     int k, rows;
     uint64_t len;
     uint32_t n_stripes;
+    uint32_t tpb;  // gathered: 2 KiB tiles per block the kernel was built for (0 = MEC_BS_TPB / rule)
 };
 
 hipError_t launch_gf8(const Gf8Launch &L, hipStream_t stream);

@@ -34,8 +34,8 @@ enum Knob : int {
     kKnobMgRows,      // MEC_MG_ROWS=3|4|8: rows per group of gf8_mg_kernel
     kKnobBitslice,    // MEC_BITSLICE=0|1|2|3: wide codes' run-time compiled kernels off / async (default) / sync / sync, every wide launch
     kKnobBsWaves,     // MEC_BS_WAVES=<n>: those kernels compiled for at least n waves per SIMD (0 = compiler's choice)
-    kKnobBsPrefetch,  // MEC_BS_PREFETCH=<n>: ... with at most n sources' loads ahead of the combine (0 = all first)
-    kKnobBsTpb,       // MEC_BS_TPB=<n>: 2 KiB tiles per block of the gathered ones (0 = rule: 4)
+    kKnobBsPrefetch,  // MEC_BS_PREFETCH=<n>: ... with at most n sources' loads ahead of the combine (unset: 4; 0 = all first)
+    kKnobBsTpb,       // MEC_BS_TPB=<n>: 2 KiB tiles per block of the gathered ones (0 = rule: 1, straight-line)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

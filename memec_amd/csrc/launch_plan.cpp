@@ -372,6 +372,11 @@ KernelPlan plan_bm_gather(const GatherLaunch &L, uint32_t s0) {
     return p;
 }
 
+uint32_t bs_gather_tpb() {
+    const int64_t kt = knob(kKnobBsTpb);
+    return kt != kKnobUnset && kt > 0 ? uint32_t(kt) : 1u;
+}
+
 KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
     KernelPlan p;
     p.k = L.k;
@@ -380,12 +385,12 @@ KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
     if (L.len == 0 || L.len % 16 || L.len > (uint64_t(1) << 32) - 2048) return fail_plan(p, "chunk size"), p;
     p.bt = kWaveBlock;
     // 2 KiB tiles (each lane two 16-byte units 1 KiB apart), tpb of them
-    // per block: gathered launches read a stripe's K + R chunk pointers
-    // once per block, so a block walks 4 tiles (VERDICT r04 item 6;
-    // MEC_BS_TPB=<n> overrides, experiments); strided blocks take one.
+    // per block.  Strided blocks take one; gathered ones the count their
+    // kernel was built for (jit.cpp: 1, straight-line like the strided
+    // kernel, unless MEC_BS_TPB asks for a loop over several tiles per
+    // pointer-row read — which measured slower, §4.7).
     const uint32_t tiles = uint32_t((L.len + 2047) / 2048);
-    const int64_t kt = knob(kKnobBsTpb);
-    p.tpb = !L.stab ? 1u : kt != kKnobUnset && kt > 0 ? uint32_t(kt) : 4u;  // strided kernels: one tile
+    p.tpb = !L.stab ? 1u : L.tpb ? L.tpb : bs_gather_tpb();
     p.tpb = std::min(p.tpb, tiles);
     p.geo.units = uint32_t(L.len / 16);
     p.geo.tiles = (tiles + p.tpb - 1) / p.tpb;

@@ -185,6 +185,8 @@ KernelPlan plan_bm_gather(const GatherLaunch &L, uint32_t s0);
 // The run-time compiled bit-sliced kernel (jit.cpp): one-wave blocks over
 // 2 KiB tiles of every chunk.
 KernelPlan plan_bs(const BsLaunch &L, uint32_t s0);
+// Tiles per block of a gathered bit-sliced kernel built now: MEC_BS_TPB, or 1.
+uint32_t bs_gather_tpb();
 // xor_kernel over len bytes.
 KernelPlan plan_xor(uint64_t len);
 

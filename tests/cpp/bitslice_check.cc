@@ -4,6 +4,10 @@
 // <= 32), the program interpreted over random 32-byte chunks equals the
 // byte-wise GF(2^8) products (0x11d), overwrite and accumulate; the emitted
 // HIP source is generated for each.  Prints "ok <programs> <ops>".
+// With a directory argument it also writes the RS(16,8)-shaped encode
+// program's kernel in its three addressing forms (strided, gathered
+// straight-line, gathered looping over tiles) as <dir>/bs_{strided,gather1,
+// gather4}.hip, for a gfx950 compile check (tests/test_abi.py).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -15,7 +19,7 @@
 
 using namespace mec;
 
-int main() {
+int main(int argc, char **argv) {
     const Field &f = Field::get(8);
     std::mt19937_64 rng(12345);
     long programs = 0, ops = 0;
@@ -63,6 +67,24 @@ int main() {
                     ++programs;
                     ops += long(p.ops.size());
                 }
+    if (argc > 1) {
+        std::vector<uint8_t> coef(8 * 16);
+        for (size_t i = 0; i < coef.size(); ++i) coef[i] = i < 16 || i % 16 == 0 ? 1 : uint8_t(rng() | 2);
+        const BsProgram p = bs_build(coef.data(), 8, 16, false);
+        const struct {
+            const char *name;
+            bool gather, loop;
+            int prefetch;
+        } forms[] = {{"strided", false, false, 4}, {"gather1", true, false, 4}, {"gather4", true, true, 4}};
+        for (const auto &fm : forms) {
+            const std::string path = std::string(argv[1]) + "/bs_" + fm.name + ".hip";
+            FILE *out = std::fopen(path.c_str(), "w");
+            if (!out) return 2;
+            const std::string src = bs_source(p, fm.gather, 0, fm.prefetch, fm.loop);
+            std::fwrite(src.data(), 1, src.size(), out);
+            std::fclose(out);
+        }
+    }
     std::printf("ok %ld %ld\n", programs, ops);
     return 0;
 }

@@ -425,9 +425,8 @@ def test_bitslice_encode_decode_update_vs_oracle(fam, knobs):
         assert np.array_equal(host(st[:, k:]), want), (fam, k, m, cs, "in place")
         base = O.fill(n * (k + m) * cs, 7100 + k + m).reshape(n, k + m, cs)  # non-codewords
         rng = np.random.default_rng(k * 100 + m)
-        for e in sorted({5, min(m, 6), m}):
-            if e > m:
-                continue
+        sizes = [e for e in sorted({5, min(m, 6), m}) if e <= m]
+        for e in sizes:
             pat = sorted(rng.choice(k + m, size=e, replace=False).tolist())
             present = sum(1 << i for i in range(k + m) if i not in pat)
             t = dev(base.copy())
@@ -450,16 +449,21 @@ def test_bitslice_encode_decode_update_vs_oracle(fam, knobs):
         want2 = np.stack([np.stack(O.encode(fam, k, m, [d2[s, jj].copy() for jj in range(k)], cs)) for s in range(n)])
         assert np.array_equal(host(par), want2), (fam, k, m, cs, "update")
         s = c.stats()
-        assert s["jit_failed"] == 0 and s["jit_kernels"] >= 4 and s["jit_launches"] >= 6, s
+        # one kernel per matrix: the encode (split and in place), each decode
+        # pattern (in place and split), the one-column update
+        assert s["jit_failed"] == 0 and s["jit_kernels"] >= 2 + len(sizes), (k, m, s)
+        assert s["jit_launches"] >= 3 + 2 * len(sizes), (k, m, s)
         c.close()
 
 
 def test_bitslice_rule(knobs):
     """MEC_BITSLICE=2: the rule (jit.cpp jit_wanted) — Vandermonde-structured
     encodes under 12 sources stay on gf8_mg_kernel, from 12 up and every
-    dense matrix (a decode) take the bit-sliced kernel; same bytes."""
+    dense matrix (a decode) take the bit-sliced kernel, unless the outputs
+    outnumber twice the sources (RS(4,12)); same bytes."""
     knobs("MEC_BITSLICE", "2")
-    for k, m, cs, want_enc in [(10, 6, 2048, False), (12, 6, 2048, True)]:
+    for k, m, cs, want_enc, want_dec in [(10, 6, 2048, False, True), (12, 6, 2048, True, True),
+                                         (4, 12, 2048, False, False)]:
         n = 2
         data = O.fill(n * k * cs, 9100 + k).reshape(n, k, cs)
         want = np.stack([np.stack(O.encode("rs", k, m, [data[s, j].copy() for j in range(k)], cs)) for s in range(n)])
@@ -476,7 +480,7 @@ def test_bitslice_rule(knobs):
         c.decode(t, sum(1 << i for i in range(k + m) if i not in pat))
         torch.cuda.synchronize()
         assert torch.equal(t, st)
-        assert c.stats()["jit_launches"] == before + 1, c.stats()
+        assert c.stats()["jit_launches"] == before + int(want_dec), c.stats()
         c.close()
 
 
@@ -511,8 +515,9 @@ def test_bitslice_async_takes_over(knobs):
 @pytest.mark.parametrize("mem", ["device", "host"])
 def test_bitslice_pointer_batch_one_map(mem, knobs):
     """Pointer batches with one map and > 4 outputs through the gathered
-    bit-sliced kernel (scattered 8-byte-aligned ChunkPool-like slots; its
-    blocks walk 4 tiles, and 1, 3 and 16 here): RS(16,8) and ISA-L
+    bit-sliced kernel (scattered 8-byte-aligned ChunkPool-like slots; one
+    straight-line 2 KiB tile per block by default, and blocks looping over
+    3 tiles under MEC_BS_TPB=3): RS(16,8) and ISA-L
     Cauchy(10,6) encode, then the same 6 erasures rebuilt in place in every
     stripe."""
     knobs("MEC_BITSLICE", "2")

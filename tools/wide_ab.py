@@ -38,9 +38,9 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
 
 ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
         "bs3": {"MEC_BITSLICE": "3", "MEC_BS_WAVES": "3"}, "bs4": {"MEC_BITSLICE": "3", "MEC_BS_WAVES": "4"},
-        "bs5": {"MEC_BITSLICE": "3", "MEC_BS_WAVES": "5"}, "bsp4": {"MEC_BITSLICE": "3", "MEC_BS_PREFETCH": "4"},
-        "bs4p4": {"MEC_BITSLICE": "3", "MEC_BS_WAVES": "4", "MEC_BS_PREFETCH": "4"},
-        "bst1": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "1"}, "bst2": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "2"},
+        "bs5": {"MEC_BITSLICE": "3", "MEC_BS_WAVES": "5"}, "bsp0": {"MEC_BITSLICE": "3", "MEC_BS_PREFETCH": "0"},
+        "bsp2": {"MEC_BITSLICE": "3", "MEC_BS_PREFETCH": "2"}, "bsp8": {"MEC_BITSLICE": "3", "MEC_BS_PREFETCH": "8"},
+        "bst4": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "4"}, "bst2": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "2"},
         "bst8": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "8"}, "bst16": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "16"},
         "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"}}
 
@@ -154,10 +154,16 @@ if __name__ == "__main__":
         rd, wr = 2 * fk * 1024, wk * 1024
         alg_r = k * cs * n
         alg_w = m * cs * n
+        # per launch too: a decode shape's setup encode moves the same bytes
+        # as each decode (k read, m written), so every coding launch counts
+        steps = a.steps + a.warmup
+        rl, wl = rd * steps / max(nf, 1), wr * steps / max(nw, 1)
         print(json.dumps({"shape": shapes[0], "arms": a.arms, "launch_rows": [nf, nw],
                           "read_bytes_per_step": rd, "write_bytes_per_step": wr,
                           "read_ratio": round(rd / alg_r, 4), "write_ratio": round(wr / alg_w, 4),
-                          "traffic_ratio": round((rd + wr) / (alg_r + alg_w), 4)}))
+                          "traffic_ratio": round((rd + wr) / (alg_r + alg_w), 4),
+                          "read_ratio_per_launch": round(rl / alg_r, 4), "write_ratio_per_launch": round(wl / alg_w, 4),
+                          "traffic_ratio_per_launch": round((rl + wl) / (alg_r + alg_w), 4)}))
     else:
         for _ in range(a.rounds):
             run(a.arms.split(","), a.steps, a.warmup, shapes)
