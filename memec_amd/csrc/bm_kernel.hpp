@@ -49,7 +49,7 @@ struct BmParams {
     uint32_t sstride, dstride, chunk, s0;
     uint64_t packet;
     uint32_t units, tiles, k, accumulate, win, pad;
-    uint32_t nstr, sgroup, srun, pad2;  // stripe-group map (stream_common.hpp stripe_tile)
+    uint32_t nstr, sgroup, srun, skew;  // stripe-group map and tile skew (stream_common.hpp stripe_tile)
     int64_t src_off[kMaxSrc];
     int64_t dst_off[R];
     uint8_t mask[kMaxSrc][R * W];
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
     typedef typename VecT<VW>::type vec;
     const uint32_t bid = block_order(p.win);
     uint32_t stripe, tile;
-    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, stripe, tile);
+    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, p.skew, stripe, tile);
     const uint32_t u = tile * BT + threadIdx.x;
     if (u >= p.units) return;
     vec acc[ROWS];
@@ -171,7 +171,7 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
     p.chunk = uint32_t(L.packet * uint64_t(L.w));
     p.accumulate = L.accumulate ? 1u : 0u;
     p.pad = 0;
-    p.pad2 = 0;
+    p.skew = 0;
     for (int j = 0; j < kMaxSrc; ++j) p.src_off[j] = j < L.k ? L.src_off[j] : 0;
     for (int i = 0; i < R; ++i) p.dst_off[i] = L.dst_off[i];
     for (int j = 0; j < kMaxSrc; ++j)
@@ -187,6 +187,7 @@ hipError_t run_bm_vw(const BmLaunch &L, hipStream_t stream) {
         p.nstr = L.stab ? 0 : pl.ns;
         p.sgroup = pl.sgroup;
         p.srun = pl.srun;
+        p.skew = pl.skew;
         p.src = L.stab ? nullptr : L.src + int64_t(s0) * L.src_stripe_stride;
         p.dst = L.stab ? nullptr : L.dst + int64_t(s0) * L.dst_stripe_stride;
         const dim3 grid(uint32_t(pl.grid)), block(pl.bt);

@@ -33,7 +33,7 @@ struct Gf8Params {
     const uint64_t *stab, *dtab;
     uint32_t sstride, dstride, chunk, s0;
     uint32_t units, tiles, accumulate, win;
-    uint32_t nstr, sgroup, srun;  // stripes in this launch, stripe group and run (stripe_tile)
+    uint32_t nstr, sgroup, srun, skew;  // stripes in this launch, stripe group and run, tile skew (stripe_tile)
     int64_t src_off[K];
     int64_t dst_off[R];
     Gf8Coef coef[R][K];
@@ -157,7 +157,7 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     __syncthreads();
     const uint32_t bid = block_order(p.win);
     uint32_t stripe, tile;
-    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, stripe, tile);
+    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, p.skew, stripe, tile);
     const uint32_t u = tile * BT + threadIdx.x;
     if (u >= p.units) return;
     // Every chunk is a buffer resource (SGPR base, 32-bit lane offsets) in
@@ -216,7 +216,7 @@ struct Gf8MgParams {
     uint64_t s0;
     uint32_t sstride, dstride;
     const uint32_t *tabs;  // device: groups x R x K x 8 dwords
-    uint32_t chunk, units, tiles, accumulate, win, nstr, sgroup, srun, groups, pad;
+    uint32_t chunk, units, tiles, accumulate, win, nstr, sgroup, srun, groups, skew;
     int64_t src_off[K];
     int64_t dst_off[kMaxSrc];  // groups x R rows; < 0 = padding
 };
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kWaveBlock) void gf8_mg_kernel(const Gf8MgParams<K>
     __syncthreads();
     const uint32_t bid = block_order(p.win);
     uint32_t stripe, tile;
-    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, stripe, tile);
+    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, p.skew, stripe, tile);
     const uint32_t u = tile * kWaveBlock + threadIdx.x;
     if (u >= p.units) return;
     const uint32_t off = u * 16;
@@ -333,6 +333,7 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
         p.nstr = L.stab ? 0 : pl.ns;
         p.sgroup = pl.sgroup;
         p.srun = pl.srun;
+        p.skew = pl.skew;
         p.src = L.stab ? nullptr : L.src + int64_t(s0) * L.src_stripe_stride;
         p.dst = L.stab ? nullptr : L.dst + int64_t(s0) * L.dst_stripe_stride;
         if (L.stab) {
@@ -365,7 +366,7 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
     p.dstride = L.dstride;
     p.chunk = uint32_t(L.len);
     p.accumulate = L.accumulate ? 1u : 0u;
-    p.pad = 0;
+    p.skew = 0;
     for (int j = 0; j < K; ++j) p.src_off[j] = L.src_off[j];
     for (uint32_t s0 = 0; s0 < L.n_stripes;) {
         const KernelPlan pl = plan_gf8_mg(L, s0);
@@ -382,6 +383,7 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
         p.nstr = L.stab ? 0 : pl.ns;
         p.sgroup = pl.sgroup;
         p.srun = pl.srun;
+        p.skew = pl.skew;
         // pointer rows: no layout to window or group over
         p.src = L.stab ? nullptr : L.src + int64_t(s0) * L.src_stripe_stride;
         p.dst = L.stab ? nullptr : L.dst + int64_t(s0) * L.dst_stripe_stride;

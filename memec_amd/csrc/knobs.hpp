@@ -36,6 +36,7 @@ enum Knob : int {
     kKnobBsWaves,     // MEC_BS_WAVES=<n>: those kernels compiled for at least n waves per SIMD (0 = compiler's choice)
     kKnobBsPrefetch,  // MEC_BS_PREFETCH=<n>: ... with at most n sources' loads ahead of the combine (unset: 4; 0 = all first)
     kKnobBsTpb,       // MEC_BS_TPB=<n>: 2 KiB tiles per block of the gathered ones (0 = rule: 1, straight-line)
+    kKnobTileSkew,    // MEC_TILE_SKEW=<tiles>: in-place strided launches rotate stripe s's tiles by s * n (0 = none)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

@@ -203,6 +203,13 @@ bool common_ok(KernelPlan &p, uint64_t lane_span_bytes) {
     return true;
 }
 uint32_t sub_stripes(const Geometry &g, uint32_t n, uint32_t s0) { return std::min(n - s0, g.max_stripes_per_launch); }
+// MEC_TILE_SKEW (experiment, default 0): in-place launches on the identity
+// map only, reduced mod the stripe's tiles
+uint32_t tile_skew(bool in_place, uint32_t sgroup, uint32_t tiles) {
+    const int64_t k = knob(kKnobTileSkew);
+    if (!in_place || sgroup != 0 || k == kKnobUnset || k <= 0 || tiles == 0) return 0;
+    return uint32_t(uint64_t(k) % tiles);
+}
 }  // namespace
 
 KernelPlan plan_gf8(const Gf8Launch &L, uint32_t s0) {
@@ -237,6 +244,7 @@ KernelPlan plan_gf8(const Gf8Launch &L, uint32_t s0) {
         const uint8_t *dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
         p.win = launch_windows(src, int64_t(p.ns) * L.src_stripe_stride, dst, int64_t(p.ns) * L.dst_stripe_stride);
         p.sgroup = stripe_group(L.len, p.geo.tiles, p.win > 1 ? p.ns / p.win : p.ns, p.win > 1, false, p.srun);
+        p.skew = tile_skew(p.win > 1, p.sgroup, p.geo.tiles);
         const bool in_place = p.win > 1;
         p.lds_dynamic = occupancy_lds(p.bt, p.bt, uint32_t(L.rows * L.k * 32),
                                       gf8_target_waves(L.k, L.rows, in_place, !vand, L.accumulate));
@@ -269,6 +277,7 @@ KernelPlan plan_gf8_mg(const Gf8MgLaunch &L, uint32_t s0) {
         const uint8_t *dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
         p.win = launch_windows(src, int64_t(p.ns) * L.src_stripe_stride, dst, int64_t(p.ns) * L.dst_stripe_stride);
         p.sgroup = stripe_group(L.len, p.geo.tiles, p.win > 1 ? p.ns / p.win : p.ns, p.win > 1, false, p.srun);
+        p.skew = tile_skew(p.win > 1, p.sgroup, p.geo.tiles);
     }
     // the tables are the block's LDS, and no wave cap: the caps of the
     // <= 4-row launches (gf8_target_waves) starve these longer-computing
@@ -324,6 +333,7 @@ KernelPlan plan_bm(const BmLaunch &L, uint32_t s0) {
         const uint8_t *dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
         p.win = bm_windows(src, int64_t(p.ns) * L.src_stripe_stride, dst, int64_t(p.ns) * L.dst_stripe_stride, cb, R, L.k);
         p.sgroup = stripe_group(cb, p.geo.tiles, p.win > 1 ? p.ns / p.win : p.ns, p.win > 1, true, p.srun);
+        p.skew = tile_skew(p.win > 1, p.sgroup, p.geo.tiles);
         const bool in_place = p.win > 1;
         p.lds_dynamic = occupancy_lds(p.bt, std::min<uint32_t>(p.bt, p.geo.units), 0,
                                       bm_target_waves(R, L.w, int(p.vw), in_place));

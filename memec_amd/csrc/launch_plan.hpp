@@ -64,6 +64,7 @@ struct KernelPlan {
     uint32_t vw = 4;         // dwords per lane (bitmatrix 2 or 4; byte-wise 4)
     uint32_t lds_static = 0, lds_dynamic = 0;
     uint32_t win = 1, sgroup = 0, srun = 8;
+    uint32_t skew = 0;       // per-stripe tile rotation (identity map, in place; MEC_TILE_SKEW)
     uint32_t tpb = 1;        // tiles per block (bit-sliced kernels: geo.tiles = blocks per stripe)
     Geometry geo{};
     uint32_t ns = 0;         // stripes in this launch

@@ -113,11 +113,16 @@ __device__ __forceinline__ uint32_t block_order(uint32_t win) {
 // stripe of the group the next 8 tiles.  group = 0 keeps the identity map;
 // tiles % run == 0 and run % 8 == 0 whenever group != 0 (host side,
 // stripe_group; `run` consecutive tiles per stripe visit, default 8).
+// skew (identity map only; MEC_TILE_SKEW, an experiment on the in-place
+// decodes): stripe s starts its tiles at s * skew mod
+// tiles, so neighbouring stripes' resident blocks sit at different column
+// offsets (a rotation per stripe: still a bijection).
 __device__ __forceinline__ void stripe_tile(uint32_t bid, uint32_t tiles, uint32_t ns, uint32_t group, uint32_t run,
-                                            uint32_t &stripe, uint32_t &tile) {
+                                            uint32_t skew, uint32_t &stripe, uint32_t &tile) {
     if (group == 0) {
         stripe = bid / tiles;
         tile = bid - stripe * tiles;
+        if (skew) tile = uint32_t((uint64_t(tile) + uint64_t(stripe) * skew) % tiles);
         return;
     }
     const uint32_t per = group * tiles;

@@ -49,6 +49,7 @@ static void common(const KernelPlan &p, uint64_t lane_span) {
     if (lane_span > (uint64_t(1) << 32)) bad("lane offsets past 32 bits", p);
     if (p.win < 1) bad("no window", p);
     if (p.sgroup != 0 && (p.srun == 0 || p.srun % 8 || p.geo.tiles % p.srun)) bad("stripe-group run", p);
+    if (p.skew != 0 && (p.sgroup != 0 || p.win < 2 || p.skew >= p.geo.tiles)) bad("tile skew off the in-place identity map", p);
 }
 
 // Synthetic layouts: split (sources and outputs in separate regions) or in

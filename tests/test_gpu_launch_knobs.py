@@ -202,3 +202,14 @@ def test_tiny_inplace_cauchy_rule(k, m, cs, knobs):
         torch.cuda.synchronize()
         assert np.array_equal(st.cpu().numpy(), base), ("in-place decode", k, m, cs, win)
     c.close()
+
+
+@pytest.mark.parametrize("skew", ["8", "64", "256"])
+@pytest.mark.parametrize("fam", ["rs", "cauchy"])
+def test_tile_skew_in_place(fam, skew, knobs):
+    """MEC_TILE_SKEW (experiment: in-place launches rotate stripe s's tiles
+    by s * skew): every layout still equals the oracle,
+    at chunks with few tiles (skew reduced mod tiles) and many."""
+    knobs("MEC_TILE_SKEW", skew)
+    for cs in (4096, 65536 + 16):
+        _check_all_layouts(fam, cs if fam == "rs" else cs - cs % 64, 900 + len(skew))
