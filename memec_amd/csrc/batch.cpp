@@ -335,7 +335,7 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
         // (gf8_kernel / bm_kernel gather mode), only the pointers are read
         const std::vector<uint8_t> &ss = M.ssel[0], &ds = M.dsel[0];
         const Mat &cf = M.coef[0];
-        if (one_pass && jit_wanted(c, ds.size(), M.K, cf)) {
+        if (one_pass && jit_wanted(c, ds.size(), M.K, cf, true)) {
             if (JitKernel *jk = jit_kernel(c, cf, ds.size(), M.K, M.accumulate, true)) {
                 BsLaunch L{};
                 L.stab = dstab;

@@ -109,25 +109,30 @@ uint64_t env_u64(const char *name, uint64_t dflt) {
 
 // Which wide launches take the bit-sliced kernel (MEC_BITSLICE unset, 1 or
 // 2): matrices with at least half as many sources as outputs that are
-// dense (decodes, ISA-L Cauchy) or have 12+ sources.  Below 12 sources a
-// Vandermonde-structured matrix (row 0 and column 0 all ones: Jerasure /
-// ISA-L RS encodes) keeps gf8_mg_kernel, whose plain-XOR row and column make
-// it cheaper there: RS(10,6)@256 KiB encode 74-75 % against 67-72, RS(8,5)
-// @16 KiB even; with fewer than half as many sources as outputs the
-// bit-sliced kernel's per-output work dominates: RS(4,12)@1 MiB encode 61
-// against 78, ISA-L Cauchy(4,12) 62 against 76.  RS(16,8) 71-74 against
-// 64-67, ISA-L RS(12,8) 79 against 65, the other dense shapes +8-24 points
-// (tools/wide_ab.py, profiles/r05/wide_ab_*.jsonl).  MEC_BITSLICE=3 takes
-// it for every wide launch (A/B), 0 never.
-bool jit_wanted(const mec_ctx *c, size_t nd, size_t ns, const Mat &coef) {
+// dense (decodes, ISA-L Cauchy), have 12+ sources, or are coded through
+// pointer rows (one-map batches).  Strided launches below 12 sources keep
+// gf8_mg_kernel for Vandermonde-structured matrices (row 0 and column 0 all
+// ones: Jerasure / ISA-L RS encodes), whose plain-XOR row and column make it
+// cheaper there: RS(10,6)@256 KiB encode 77.7 % against 70.5, RS(8,5)@16
+// KiB 80.1 against 71.4 — but through pointer rows the gathered one-pass
+// kernel loses that lead (RS(10,6) batch 71.7 against 79.1).  With fewer
+// than half as many sources as outputs the bit-sliced kernel's per-output
+// work dominates: RS(4,12)@1 MiB encode 61 against 79, ISA-L Cauchy(4,12)
+// 63 against 75 (its in-place RS(4,12) decode of 12 is the exception, 81
+// against 75).  Elsewhere +4-24 points: RS(16,8) 72.8 against 68.8, ISA-L
+// RS(12,8) 77.5 against 68.8, 8-erasure decode 77.0 against 56.9
+// (tools/wide_ab.py, profiles/r05/wide_ab_*.jsonl).  MEC_BITSLICE=3 takes it
+// for every wide launch (A/B), 0 never.
+bool jit_wanted(const mec_ctx *c, size_t nd, size_t ns, const Mat &coef, bool gathered) {
     const int64_t kn = detail::knob(detail::kKnobBitslice);
     if (kn == 0 || !c->byte_wise() || nd <= size_t(kMaxRows) || c->cs % 16 != 0) return false;
     if (kn == 3) return true;
     if (nd > 2 * ns) return false;
+    if (gathered || ns >= 12) return true;
     bool vand = true;
     for (size_t j = 0; j < ns && vand; ++j) vand = coef[j] == 1;
     for (size_t r = 0; r < nd && vand; ++r) vand = coef[r * ns] == 1;
-    return !vand || ns >= 12;
+    return !vand;
 }
 
 // The kernel for (coef, accumulate, addressing), compiling it if needed;

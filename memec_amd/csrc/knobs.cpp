@@ -16,7 +16,7 @@ namespace {
 // limit); windows 1..16; MEC_SGROUP groups 0..64 stripes (0 / 1 = identity
 // map) with runs of 8..1024 tiles in steps of 8 (stripe_tile's contract).
 constexpr KnobSpec kSpecs[] = {
-    {"MEC_SGROUP", kKnobSgroup, 0, 64, {}, 0},
+    {"MEC_SGROUP", kKnobSgroup, 0, 64, {}, 0, 0},
     {"MEC_WINDOWS", kKnobWindows, 1, 16, {}, 0},
     {"MEC_BLOCK", kKnobBlock, 64, 256, {64, 256}, 2},
     {"MEC_GBLOCK", kKnobGblock, 64, 256, {64, 256}, 2},
@@ -30,7 +30,7 @@ constexpr KnobSpec kSpecs[] = {
     {"MEC_BS_WAVES", kKnobBsWaves, 0, 8, {}, 0},
     {"MEC_BS_PREFETCH", kKnobBsPrefetch, 0, 31, {}, 0},
     {"MEC_BS_TPB", kKnobBsTpb, 0, 64, {}, 0},
-    {"MEC_TILE_SKEW", kKnobTileSkew, 0, 256, {0, 8, 64, 256}, 4},
+    {"MEC_TILE_SKEW", kKnobTileSkew, 0, 1024, {}, 0, 8},
 };
 // every knob but MEC_SGROUP's run half has its own variable
 static_assert(sizeof(kSpecs) / sizeof(kSpecs[0]) == kKnobCount - 1, "a knob whose variable is never read");
@@ -53,6 +53,7 @@ bool parse_int(const char *s, const char *end, int64_t &out) {
 
 bool accepted(const KnobSpec &s, int64_t v) {
     if (v < s.lo || v > s.hi) return false;
+    if (s.step > 1 && (v - s.lo) % s.step != 0) return false;
     if (s.nset == 0) return true;
     for (int i = 0; i < s.nset; ++i)
         if (s.set[i] == v) return true;

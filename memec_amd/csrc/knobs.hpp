@@ -36,19 +36,20 @@ enum Knob : int {
     kKnobBsWaves,     // MEC_BS_WAVES=<n>: those kernels compiled for at least n waves per SIMD (0 = compiler's choice)
     kKnobBsPrefetch,  // MEC_BS_PREFETCH=<n>: ... with at most n sources' loads ahead of the combine (unset: 4; 0 = all first)
     kKnobBsTpb,       // MEC_BS_TPB=<n>: 2 KiB tiles per block of the gathered ones (0 = rule: 1, straight-line)
-    kKnobTileSkew,    // MEC_TILE_SKEW=<tiles>: in-place strided launches rotate stripe s's tiles by s * n (0 = none)
+    kKnobTileSkew,    // MEC_TILE_SKEW=<tiles>: strided identity-map launches rotate stripe s's tiles by s * n (0 = none; unset = rule)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;
 
-// Accepted values of one knob: lo..hi, and when `set` is non-empty only the
-// values it lists (terminated by 0 unless 0 itself is listed first).
+// Accepted values of one knob: lo..hi in steps of `step` (0 = 1), and when
+// `set` is non-empty only the values it lists.
 struct KnobSpec {
     const char *name;  // environment variable
     Knob knob;
     int64_t lo, hi;
     int64_t set[4];
     int nset;
+    int64_t step;
 };
 // The table (knobs.cpp); MEC_SGROUP's run half is checked with it.
 const KnobSpec *knob_specs(int &n);

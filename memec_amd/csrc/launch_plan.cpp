@@ -203,12 +203,14 @@ bool common_ok(KernelPlan &p, uint64_t lane_span_bytes) {
     return true;
 }
 uint32_t sub_stripes(const Geometry &g, uint32_t n, uint32_t s0) { return std::min(n - s0, g.max_stripes_per_launch); }
-// MEC_TILE_SKEW (experiment, default 0): in-place launches on the identity
-// map only, reduced mod the stripe's tiles
+// Per-stripe tile rotation of identity-map strided launches
+// (stream_common.hpp stripe_tile): in place, kTileSkew tiles; split
+// layouts none.  MEC_TILE_SKEW=<n> forces n (0 = none) on either.
 uint32_t tile_skew(bool in_place, uint32_t sgroup, uint32_t tiles) {
     const int64_t k = knob(kKnobTileSkew);
-    if (!in_place || sgroup != 0 || k == kKnobUnset || k <= 0 || tiles == 0) return 0;
-    return uint32_t(uint64_t(k) % tiles);
+    const int64_t v = k != kKnobUnset ? k : in_place ? kTileSkew : 0;
+    if (sgroup != 0 || v <= 0 || tiles == 0) return 0;
+    return uint32_t(uint64_t(v) % tiles);
 }
 }  // namespace
 

@@ -25,6 +25,9 @@ constexpr int kWaveBlock = 64;
 constexpr int64_t kWaveBlockSpan = int64_t(8) << 20;
 constexpr uint64_t kBmWaveChunk = uint64_t(256) << 10;
 constexpr uint32_t kLdsPerCu = 160u << 10;  // gfx950: one block may take all of it
+// In-place strided launches rotate stripe s's tiles by s * kTileSkew
+// (DESIGN §5.3); 0 keeps the identity order.
+constexpr int64_t kTileSkew = 0;
 
 // Matrix structure a gf8 launch is specialised for (gf8_kernel.hpp).
 constexpr int kGf8Dense = 0;

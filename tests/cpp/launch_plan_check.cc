@@ -49,7 +49,7 @@ static void common(const KernelPlan &p, uint64_t lane_span) {
     if (lane_span > (uint64_t(1) << 32)) bad("lane offsets past 32 bits", p);
     if (p.win < 1) bad("no window", p);
     if (p.sgroup != 0 && (p.srun == 0 || p.srun % 8 || p.geo.tiles % p.srun)) bad("stripe-group run", p);
-    if (p.skew != 0 && (p.sgroup != 0 || p.win < 2 || p.skew >= p.geo.tiles)) bad("tile skew off the in-place identity map", p);
+    if (p.skew != 0 && (p.sgroup != 0 || p.skew >= p.geo.tiles)) bad("tile skew off the identity map", p);
 }
 
 // Synthetic layouts: split (sources and outputs in separate regions) or in
@@ -307,7 +307,7 @@ static std::vector<std::string> values_of(const KnobSpec &s) {
     if (s.nset) {
         for (int i = 0; i < s.nset; ++i) v.push_back(std::to_string(s.set[i]));
     } else {
-        for (int64_t x = s.lo; x <= s.hi; ++x) v.push_back(std::to_string(x));
+        for (int64_t x = s.lo; x <= s.hi; x += s.step > 1 ? s.step : 1) v.push_back(std::to_string(x));
     }
     if (s.knob == kKnobSgroup) {  // with run lengths
         std::vector<std::string> r;
@@ -358,7 +358,8 @@ int main(int argc, char **argv) {
     // values outside the accepted sets are refused
     const char *refused[][2] = {{"MEC_MG_ROWS", "5"}, {"MEC_MG_ROWS", "2"}, {"MEC_BLOCK", "128"}, {"MEC_WPC", "33"},
                                 {"MEC_WPC", "-1"},   {"MEC_WINDOWS", "0"}, {"MEC_SGROUP", "4:7"}, {"MEC_SGROUP", "bad"},
-                                {"MEC_BM_VW", "3"},  {"MEC_WIDE", "2"},    {"MEC_WPC", "12x"}};
+                                {"MEC_BM_VW", "3"},  {"MEC_WIDE", "2"},    {"MEC_WPC", "12x"},
+                                {"MEC_TILE_SKEW", "12"}, {"MEC_TILE_SKEW", "2048"}};
     for (auto &r : refused)
         if (set_knob(r[0], r[1]) != KnobStatus::kInvalid) {
             std::printf("VIOLATION %s=%s accepted\n", r[0], r[1]);

@@ -460,9 +460,10 @@ def test_bitslice_encode_decode_update_vs_oracle(fam, knobs):
 
 def test_bitslice_rule(knobs):
     """MEC_BITSLICE=2: the rule (jit.cpp jit_wanted) — Vandermonde-structured
-    encodes under 12 sources stay on gf8_mg_kernel, from 12 up and every
-    dense matrix (a decode) take the bit-sliced kernel, unless the outputs
-    outnumber twice the sources (RS(4,12)); same bytes."""
+    encodes under 12 sources stay on gf8_mg_kernel when strided, from 12 up,
+    every dense matrix (a decode) and every one-map pointer batch take the
+    bit-sliced kernel, unless the outputs outnumber twice the sources
+    (RS(4,12)); same bytes."""
     knobs("MEC_BITSLICE", "2")
     for k, m, cs, want_enc, want_dec in [(10, 6, 2048, False, True), (12, 6, 2048, True, True),
                                          (4, 12, 2048, False, False)]:
@@ -471,7 +472,8 @@ def test_bitslice_rule(knobs):
         want = np.stack([np.stack(O.encode("rs", k, m, [data[s, j].copy() for j in range(k)], cs)) for s in range(n)])
         c = Codec("rs", k, m, cs)
         par = torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)
-        c.encode(dev(data), par)
+        data_t = dev(data)
+        c.encode(data_t, par)
         assert np.array_equal(host(par), want)
         assert (c.stats()["jit_launches"] == 1) == want_enc, (k, m, c.stats())
         st = torch.cat([dev(data), par], dim=1)
@@ -483,6 +485,15 @@ def test_bitslice_rule(knobs):
         torch.cuda.synchronize()
         assert torch.equal(t, st)
         assert c.stats()["jit_launches"] == before + int(want_dec), c.stats()
+        # through pointer rows (a one-map batch) Vandermonde matrices under
+        # 12 sources take it too, unless outputs exceed twice the sources
+        par2 = torch.zeros_like(par)
+        before = c.stats()["jit_launches"]
+        c.encode_batch([data_t[s, j].data_ptr() for s in range(n) for j in range(k)],
+                       [par2[s, i].data_ptr() for s in range(n) for i in range(m)], mem="device")
+        torch.cuda.synchronize()
+        assert torch.equal(par2, par)
+        assert c.stats()["jit_launches"] == before + int(m <= 2 * k), (k, m, c.stats())
         c.close()
 
 
