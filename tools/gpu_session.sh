@@ -80,6 +80,12 @@ for step in "$@"; do
             done ;;
         wide) run wide_ab 600 python tools/wide_ab.py --bytewise --arms bs,mg --steps 10 ;;
         server) run server_pattern 900 bash tools/server_pattern.sh ;;
+        zc)  # zero-copy single-stripe decodes in place, every call's bytes checked (tools/zc_stress.py)
+            for a in "rs 65536 0" "cauchy 65536 0" "rs 65536 8" "rs 4096 0"; do
+                set -- $a
+                run "zc_$1_$2_q$3" 300 python3 tools/zc_stress.py --fam $1 --cs $2 --queue $3 --iters ${ZC_ITERS:-3000}
+                grep -h '^{' "$OUT/zc_$1_$2_q$3.log" >> "$OUT/zc_stress.jsonl"
+            done ;;
         tsan)  # host-TSan build (tools/tsan_build.sh, built beforehand): concurrent callers
             export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 exitcode=0 suppressions=$PWD/tools/tsan_suppressions.txt"
             for c in rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536; do

@@ -6,7 +6,7 @@ zero = the GPU's stores to host memory not yet visible; other bytes =
 wrong data).  Round-5 investigation of one mismatch in the full GPU suite
 (profiles/r05/parity/pytest_gpu_r05a_zc_mismatch.log).
 
-  python tools/zc_stress.py [--iters N] [--fam rs] [--cs 65536]
+  python tools/zc_stress.py [--iters N] [--fam rs] [--cs 65536] [--queue SLOTS]
 """
 import argparse
 import json
@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--cs", type=int, default=65536)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--queue", type=int, default=0, help="resident queue slots (0: per-call launches, as the test)")
     a = ap.parse_args()
     k, m, cs = a.k, a.m, a.cs
     slot = cs + 8
@@ -40,6 +41,8 @@ def main():
     host_register(buf)
     view = [buf[i * slot + 8:i * slot + 8 + cs] for i in range(k + m)]
     c = Codec(a.fam, k, m, cs)
+    if a.queue:
+        c.set_host_queue(a.queue)
     data = [view[j] for j in range(k)]
     par = O.encode(a.fam, k, m, [d.copy() for d in data], cs)
     for i in range(m):
@@ -67,8 +70,9 @@ def main():
     st = c.stats()
     c.close()
     host_unregister(buf)
-    print(json.dumps({"fam": a.fam, "k": k, "m": m, "cs": cs, "iters": a.iters, **bad, "first": first,
-                      "zero_copy_calls": st["zero_copy_calls"], "staged_calls": st["staged_calls"]}), flush=True)
+    print(json.dumps({"fam": a.fam, "k": k, "m": m, "cs": cs, "iters": a.iters, "queue": a.queue, **bad, "first": first,
+                      "zero_copy_calls": st["zero_copy_calls"], "staged_calls": st["staged_calls"],
+                      "queue_calls": st["queue_calls"]}), flush=True)
 
 
 if __name__ == "__main__":
