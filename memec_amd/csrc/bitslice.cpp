@@ -4,6 +4,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <string>
 
 #include "gf_math.hpp"
 
@@ -178,7 +179,7 @@ void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out) 
     }
 }
 
-std::string bs_source(const BsProgram &p, bool gather, int waves, int prefetch, bool loop) {
+std::string bs_source(const BsProgram &p, bool gather, int waves, int prefetch, bool loop, bool fence) {
     std::string s;
     s.reserve(p.ops.size() * 48 + 4096);
     s += gather ? "#define MEC_GATHER 1\n" : "#define MEC_GATHER 0\n";
@@ -240,9 +241,47 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
     // once would be 96 SGPRs and spill into VGPR lanes)
     auto emit_load = [&](int j) {
         std::snprintf(buf, sizeof buf,
-                      "    const u32x4 sa%d = LD(mec_rsrc(sp%d, p.chunk), off), sb%d = LD(mec_rsrc(sp%d, p.chunk), off + 1024u);\n",
+                      "    u32x4 sa%d = LD(mec_rsrc(sp%d, p.chunk), off), sb%d = LD(mec_rsrc(sp%d, p.chunk), off + 1024u);\n",
                       j, j, j, j);
         s += buf;
+    };
+    // value names (renamed at fences) and each value's last use
+    std::vector<std::string> nm(p.ops.size());
+    std::vector<size_t> last(p.ops.size(), 0);
+    for (size_t i = 0; i < p.ops.size(); ++i) {
+        nm[i] = "v" + std::to_string(i);
+        const BsOp &o = p.ops[i];
+        auto use = [&](int x) {
+            if (x >= 0) last[size_t(x)] = i;
+        };
+        switch (o.op) {
+            case BsOpc::kShl:
+            case BsOpc::kShr: use(o.a); break;
+            case BsOpc::kBfi:
+            case BsOpc::kXor2: use(o.a); use(o.b); break;
+            case BsOpc::kXor3: use(o.a); use(o.b); use(o.c); break;
+            case BsOpc::kStore: use(o.a); break;
+            default: break;
+        }
+    }
+    int nfence = 0;
+    auto emit_fence = [&](size_t i0, int j) {  // before op i0, where source j starts
+        std::vector<size_t> live;
+        for (size_t x = 0; x < i0; ++x)
+            if (p.ops[x].op != BsOpc::kStore && last[x] >= i0) live.push_back(x);
+        for (size_t g = 0; g < live.size(); g += 8) {
+            std::string decl, cons;
+            for (size_t t = g; t < live.size() && t < g + 8; ++t) {
+                const std::string w = "f" + std::to_string(nfence) + "_" + std::to_string(live[t]);
+                decl += "    u32 " + w + " = " + nm[live[t]] + ";\n";
+                cons += std::string(cons.empty() ? "" : ", ") + "\"+v\"(" + w + ")";
+                nm[live[t]] = w;
+            }
+            s += decl + "    __asm__ volatile(\"\" : " + cons + ");\n";
+        }
+        std::snprintf(buf, sizeof buf, "    __asm__ volatile(\"\" : \"+v\"(sa%d), \"+v\"(sb%d));\n", j, j);
+        s += buf;
+        ++nfence;
     };
     // (gathered: the pointer-row entry is re-read per tile, from the scalar
     // cache after the block's first tile; holding all K + R pointers across
@@ -283,6 +322,8 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
         if (o.op == BsOpc::kLoad && o.b == 0 && o.a > 0 && next_load < p.ns && next_load <= o.a + depth - 1) {
             emit_load(next_load++);  // source o.a starts: keep `depth` sources in flight
         }
+        if (fence && o.op == BsOpc::kLoad && o.b == 0 && o.a > 0) emit_fence(i, o.a);
+        auto N = [&](int x) { return nm[size_t(x)].c_str(); };
         switch (o.op) {
             case BsOpc::kLoad:
                 std::snprintf(buf, sizeof buf, "    const u32 v%zu = s%c%d.%c;\n", i, o.b < 4 ? 'a' : 'b', o.a, comp[o.b & 3]);
@@ -290,19 +331,19 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
             case BsOpc::kLoadOut:
                 std::snprintf(buf, sizeof buf, "    const u32 v%zu = o%c%d.%c;\n", i, o.b < 4 ? 'a' : 'b', o.a, comp[o.b & 3]);
                 break;
-            case BsOpc::kShl: std::snprintf(buf, sizeof buf, "    const u32 v%zu = v%d << %u;\n", i, o.a, o.imm); break;
-            case BsOpc::kShr: std::snprintf(buf, sizeof buf, "    const u32 v%zu = v%d >> %u;\n", i, o.a, o.imm); break;
+            case BsOpc::kShl: std::snprintf(buf, sizeof buf, "    const u32 v%zu = %s << %u;\n", i, N(o.a), o.imm); break;
+            case BsOpc::kShr: std::snprintf(buf, sizeof buf, "    const u32 v%zu = %s >> %u;\n", i, N(o.a), o.imm); break;
             case BsOpc::kBfi:
-                std::snprintf(buf, sizeof buf, "    const u32 v%zu = BFI(0x%08xu, v%d, v%d);\n", i, o.imm, o.a, o.b);
+                std::snprintf(buf, sizeof buf, "    const u32 v%zu = BFI(0x%08xu, %s, %s);\n", i, o.imm, N(o.a), N(o.b));
                 break;
             case BsOpc::kXor2:
                 if (o.a < 0)
                     std::snprintf(buf, sizeof buf, "    const u32 v%zu = 0u;\n", i);
                 else
-                    std::snprintf(buf, sizeof buf, "    const u32 v%zu = v%d ^ v%d;\n", i, o.a, o.b);
+                    std::snprintf(buf, sizeof buf, "    const u32 v%zu = %s ^ %s;\n", i, N(o.a), N(o.b));
                 break;
             case BsOpc::kXor3:
-                std::snprintf(buf, sizeof buf, "    const u32 v%zu = X3(v%d, v%d, v%d);\n", i, o.a, o.b, o.c);
+                std::snprintf(buf, sizeof buf, "    const u32 v%zu = X3(%s, %s, %s);\n", i, N(o.a), N(o.b), N(o.c));
                 break;
             case BsOpc::kStore: {
                 stored[size_t(o.b)][size_t(o.c)] = o.a;
@@ -312,9 +353,9 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
                 if (all) {
                     const std::vector<int> &w = stored[size_t(o.b)];
                     std::snprintf(buf, sizeof buf,
-                                  "    mec_st(v%d, v%d, v%d, v%d, mec_rsrc(dp%d, p.chunk), off);\n"
-                                  "    mec_st(v%d, v%d, v%d, v%d, mec_rsrc(dp%d, p.chunk), off + 1024u);\n",
-                                  w[0], w[1], w[2], w[3], o.b, w[4], w[5], w[6], w[7], o.b);
+                                  "    mec_st(%s, %s, %s, %s, mec_rsrc(dp%d, p.chunk), off);\n"
+                                  "    mec_st(%s, %s, %s, %s, mec_rsrc(dp%d, p.chunk), off + 1024u);\n",
+                                  N(w[0]), N(w[1]), N(w[2]), N(w[3]), o.b, N(w[4]), N(w[5]), N(w[6]), N(w[7]), o.b);
                 }
                 break;
             }

@@ -71,7 +71,13 @@ void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out);
 // combine (0: every load first).
 // loop (gathered only): the block walks p.tpb tiles per pointer-row read;
 // otherwise it codes one tile, straight-line (launch with tpb = 1).
-std::string bs_source(const BsProgram &p, bool gather, int waves = 0, int prefetch = 0, bool loop = false);
+// fence: between sources, an empty asm that takes every value live across
+// the boundary (the output planes' running XORs) and the next source's
+// loaded units, so the compiler cannot start a source's transposes and
+// combinations before the previous source's are consumed (one source's
+// combinations live at a time).
+std::string bs_source(const BsProgram &p, bool gather, int waves = 0, int prefetch = 0, bool loop = false,
+                      bool fence = false);
 
 // Kernel arguments of every generated kernel (the same layout in the
 // generated source, bs_source).  Strided: source j of stripe s at src + s *

@@ -158,6 +158,12 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     const int64_t pk = detail::knob(detail::kKnobBsPrefetch);
     const int prefetch = pk == detail::kKnobUnset ? 4 : int(pk);
     key += char(prefetch);
+    // scheduling fences between sources: one source's combinations live at
+    // a time — RS(16,8) 141 -> 127 VGPRs strided, 167 -> 127 gathered, i.e.
+    // 4 waves per SIMD instead of 3 (bitslice.hpp)
+    const int64_t fk = detail::knob(detail::kKnobBsFence);
+    const bool fence = fk == detail::kKnobUnset ? true : fk != 0;
+    key += char(fence ? 1 : 0);
     JitCache &J = c->jit;
     const bool sync = detail::knob(detail::kKnobBitslice) >= 2;
     std::shared_ptr<JitKernel> k;
@@ -177,7 +183,7 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
         }
     }
     if (fresh) {
-        auto src = std::make_shared<std::string>(bs_source(bs_build(coef.data(), int(nd), int(ns), accumulate), gather, waves, prefetch, loop));
+        auto src = std::make_shared<std::string>(bs_source(bs_build(coef.data(), int(nd), int(ns), accumulate), gather, waves, prefetch, loop, fence));
         const int device = c->device;
         auto done = [&J, k] {
             std::lock_guard<std::mutex> g(J.mu);

@@ -6,8 +6,9 @@
 // HIP source is generated for each.  Prints "ok <programs> <ops>".
 // With a directory argument it also writes the RS(16,8)-shaped encode
 // program's kernel in its three addressing forms (strided, gathered
-// straight-line, gathered looping over tiles) as <dir>/bs_{strided,gather1,
-// gather4}.hip, for a gfx950 compile check (tests/test_abi.py).
+// straight-line, gathered looping over tiles), with the default scheduling
+// fences, and the strided form without them, as <dir>/bs_{strided,gather1,
+// gather4,strided_nofence}.hip, for a gfx950 compile check (tests/test_abi.py).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -75,12 +76,14 @@ int main(int argc, char **argv) {
             const char *name;
             bool gather, loop;
             int prefetch;
-        } forms[] = {{"strided", false, false, 4}, {"gather1", true, false, 4}, {"gather4", true, true, 4}};
+            bool fence;
+        } forms[] = {{"strided", false, false, 4, true}, {"gather1", true, false, 4, true},
+                     {"gather4", true, true, 4, true}, {"strided_nofence", false, false, 4, false}};
         for (const auto &fm : forms) {
             const std::string path = std::string(argv[1]) + "/bs_" + fm.name + ".hip";
             FILE *out = std::fopen(path.c_str(), "w");
             if (!out) return 2;
-            const std::string src = bs_source(p, fm.gather, 0, fm.prefetch, fm.loop);
+            const std::string src = bs_source(p, fm.gather, 0, fm.prefetch, fm.loop, fm.fence);
             std::fwrite(src.data(), 1, src.size(), out);
             std::fclose(out);
         }

@@ -42,6 +42,7 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "bsp2": {"MEC_BITSLICE": "3", "MEC_BS_PREFETCH": "2"}, "bsp8": {"MEC_BITSLICE": "3", "MEC_BS_PREFETCH": "8"},
         "bst4": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "4"}, "bst2": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "2"},
         "bst8": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "8"}, "bst16": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "16"},
+        "bsnf": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0"}, "autonf": {"MEC_BITSLICE": "2", "MEC_BS_FENCE": "0"},
         "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"}}
 
 
