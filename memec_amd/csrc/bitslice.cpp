@@ -154,6 +154,27 @@ BsProgram bs_build(const uint8_t *coef, int nd, int ns, bool accumulate) {
     return B.p;
 }
 
+BsProgram bs_build_twin(int nd, int ns, bool accumulate) {
+    Builder B;
+    B.p.ns = ns;
+    B.p.nd = nd;
+    B.p.accumulate = accumulate;
+    int x[8];
+    for (int j = 0; j < ns; ++j) {
+        for (int d = 0; d < 8; ++d) {
+            const int v = B.emit(BsOpc::kLoad, j, d);
+            x[d] = j == 0 ? v : B.emit(BsOpc::kXor2, x[d], v);
+        }
+    }
+    for (int r = 0; r < nd; ++r)
+        for (int d = 0; d < 8; ++d) {
+            int v = x[d];
+            if (accumulate) v = B.emit(BsOpc::kXor2, v, B.emit(BsOpc::kLoadOut, r, d));
+            B.emit(BsOpc::kStore, v, r, d);
+        }
+    return B.p;
+}
+
 void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out) {
     std::vector<uint32_t> v(p.ops.size(), 0);
     auto dword = [](const uint8_t *b, int d) {

@@ -60,6 +60,11 @@ struct BsProgram {
 // The program for outputs (^)= coef (nd x ns, row-major over GF(2^8) with
 // the 0x11d polynomial) * sources.
 BsProgram bs_build(const uint8_t *coef, int nd, int ns, bool accumulate);
+// The arithmetic-free twin of a bs_build program (mec_set_probe): the same
+// loads and stores, every output the plain XOR of the sources (8 dwords x
+// ns / 2 three-input XORs), so a launch measures what the access pattern
+// alone sustains.  Not a code.
+BsProgram bs_build_twin(int nd, int ns, bool accumulate);
 // CPU interpreter: src = ns chunks of 32 bytes, out = nd chunks of 32 bytes
 // (read too when accumulating).  Bytes [0, 16) are unit 0, [16, 32) unit 1.
 void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out);

@@ -137,7 +137,7 @@ bool jit_wanted(const mec_ctx *c, size_t nd, size_t ns, const Mat &coef, bool ga
 
 // The kernel for (coef, accumulate, addressing), compiling it if needed;
 // nullptr while it compiles (async), past the cap, or after a failure.
-JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool accumulate, bool gather) {
+JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool accumulate, bool gather, bool twin) {
     std::string key(reinterpret_cast<const char *>(coef.data()), nd * ns);
     key += char(nd);
     key += char(ns);
@@ -164,6 +164,7 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     const int64_t fk = detail::knob(detail::kKnobBsFence);
     const bool fence = fk == detail::kKnobUnset ? true : fk != 0;
     key += char(fence ? 1 : 0);
+    key += char(twin ? 1 : 0);
     JitCache &J = c->jit;
     const bool sync = detail::knob(detail::kKnobBitslice) >= 2;
     std::shared_ptr<JitKernel> k;
@@ -183,7 +184,8 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
         }
     }
     if (fresh) {
-        auto src = std::make_shared<std::string>(bs_source(bs_build(coef.data(), int(nd), int(ns), accumulate), gather, waves, prefetch, loop, fence));
+        auto src = std::make_shared<std::string>(bs_source(twin ? bs_build_twin(int(nd), int(ns), accumulate) : bs_build(coef.data(), int(nd), int(ns), accumulate),
+                      gather, waves, prefetch, loop, fence));
         const int device = c->device;
         auto done = [&J, k] {
             std::lock_guard<std::mutex> g(J.mu);

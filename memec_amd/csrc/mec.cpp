@@ -148,9 +148,10 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
         return MEC_OK;
     }
     const bool probe = c->probe.load(std::memory_order_relaxed) == MEC_PROBE_XOR;
-    if (!probe && jit_wanted(c, nd, ns, coef, false)) {
+    if (jit_wanted(c, nd, ns, coef, false)) {
         // more than 4 outputs: the matrix's own bit-sliced kernel once built
-        if (JitKernel *jk = jit_kernel(c, coef, nd, ns, accumulate, false)) {
+        // (its arithmetic-free twin under MEC_PROBE_XOR)
+        if (JitKernel *jk = jit_kernel(c, coef, nd, ns, accumulate, false, probe)) {
             mec::BsLaunch L{};
             L.src = lay.src;
             L.dst = lay.dst;

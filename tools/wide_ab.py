@@ -43,7 +43,10 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "bst4": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "4"}, "bst2": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "2"},
         "bst8": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "8"}, "bst16": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "16"},
         "bsnf": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0"}, "autonf": {"MEC_BITSLICE": "2", "MEC_BS_FENCE": "0"},
-        "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"}}
+        "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"},
+        # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
+        "bstwin": {"MEC_BITSLICE": "3", "PROBE": "xor"}, "bsnftwin": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0", "PROBE": "xor"}}
+KNOBS = sorted({kn for a in ARMS.values() for kn in a if kn.startswith("MEC_")})
 
 
 def run(arms_list, steps, warmup, shapes):
@@ -89,8 +92,9 @@ def run(arms_list, steps, warmup, shapes):
             result = lambda: st[:, erased]  # noqa: E731
         arms = {}
         for arm in arms_list:
-            for kn in ("MEC_BITSLICE", "MEC_WIDE", "MEC_BS_WAVES", "MEC_BS_PREFETCH", "MEC_BS_TPB"):
+            for kn in KNOBS:  # every knob any arm sets: unset unless this arm sets it
                 memec_amd.set_knob(kn, ARMS[arm].get(kn))
+            c.set_probe(ARMS[arm].get("PROBE") == "xor")
             for _ in range(warmup):
                 step()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -103,12 +107,13 @@ def run(arms_list, steps, warmup, shapes):
             arms[arm] = {"ms_per_step": round(ms, 4), "GBps": round(alg / (ms * 1e-3) / 1e9, 1),
                          "frac": round(alg / (ms * 1e-3) / 8e12, 4)}
             arms[arm]["digest"] = int(result().view(torch.int64).sum().item())
-        for kn in ("MEC_BITSLICE", "MEC_WIDE", "MEC_BS_WAVES", "MEC_BS_PREFETCH", "MEC_BS_TPB"):
+        for kn in KNOBS:
             memec_amd.set_knob(kn, None)
+        c.set_probe(False)
         rec = {"family": fam, "k": k, "m": m, "chunk": cs, "stripes": n, "op": op, "alg_bytes": alg, **arms}
         if op == "decode":
             rec["restored"] = bool(torch.equal(result(), orig))
-        rec["equal"] = len({arms[a]["digest"] for a in arms_list}) == 1
+        rec["equal"] = len({arms[a]["digest"] for a in arms_list if "PROBE" not in ARMS[a]}) == 1
         rec["jit"] = {x: c.stats()[x] for x in ("jit_kernels", "jit_launches", "jit_compile_ms", "jit_failed")}
         print(json.dumps(rec), flush=True)
         out.append(rec)
