@@ -158,11 +158,14 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     const int64_t pk = detail::knob(detail::kKnobBsPrefetch);
     const int prefetch = pk == detail::kKnobUnset ? 4 : int(pk);
     key += char(prefetch);
-    // scheduling fences between sources: one source's combinations live at
-    // a time — RS(16,8) 141 -> 127 VGPRs strided, 167 -> 127 gathered, i.e.
-    // 4 waves per SIMD instead of 3 (bitslice.hpp)
+    // scheduling fences between sources (bitslice.hpp): one source's
+    // combinations live at a time.  Gathered kernels take them — RS(16,8)
+    // 167 -> 127 VGPRs, 3 -> 4 waves per SIMD, one-map batches +2-5 points;
+    // strided ones do not — 141 -> 127 VGPRs there loses 1-4 points on the
+    // encodes (more waves only lengthen the memory queue;
+    // profiles/r05/wide_fence_twin_box7.jsonl)
     const int64_t fk = detail::knob(detail::kKnobBsFence);
-    const bool fence = fk == detail::kKnobUnset ? true : fk != 0;
+    const bool fence = fk == detail::kKnobUnset ? gather : fk != 0;
     key += char(fence ? 1 : 0);
     key += char(twin ? 1 : 0);
     JitCache &J = c->jit;

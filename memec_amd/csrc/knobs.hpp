@@ -37,7 +37,7 @@ enum Knob : int {
     kKnobBsPrefetch,  // MEC_BS_PREFETCH=<n>: ... with at most n sources' loads ahead of the combine (unset: 4; 0 = all first)
     kKnobBsTpb,       // MEC_BS_TPB=<n>: 2 KiB tiles per block of the gathered ones (0 = rule: 1, straight-line)
     kKnobTileSkew,    // MEC_TILE_SKEW=<tiles>: strided identity-map launches rotate stripe s's tiles by s * n (0 = none; unset = rule)
-    kKnobBsFence,     // MEC_BS_FENCE=0|1: bit-sliced kernels compiled with scheduling fences between sources (unset: 1)
+    kKnobBsFence,     // MEC_BS_FENCE=0|1: bit-sliced kernels compiled with scheduling fences between sources (unset: gathered ones)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

@@ -5,10 +5,11 @@
 // byte-wise GF(2^8) products (0x11d), overwrite and accumulate; the emitted
 // HIP source is generated for each.  Prints "ok <programs> <ops>".
 // With a directory argument it also writes the RS(16,8)-shaped encode
-// program's kernel in its three addressing forms (strided, gathered
-// straight-line, gathered looping over tiles), with the default scheduling
-// fences, and the strided form without them, as <dir>/bs_{strided,gather1,
-// gather4,strided_nofence}.hip, for a gfx950 compile check (tests/test_abi.py).
+// program's kernel in its three addressing forms as the JIT builds them by
+// default (strided without scheduling fences, gathered straight-line and
+// gathered looping over tiles with them), and the strided form with fences,
+// as <dir>/bs_{strided,gather1,gather4,strided_fence}.hip, for a gfx950
+// compile check (tests/test_abi.py).
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -77,8 +78,8 @@ int main(int argc, char **argv) {
             bool gather, loop;
             int prefetch;
             bool fence;
-        } forms[] = {{"strided", false, false, 4, true}, {"gather1", true, false, 4, true},
-                     {"gather4", true, true, 4, true}, {"strided_nofence", false, false, 4, false}};
+        } forms[] = {{"strided", false, false, 4, false}, {"gather1", true, false, 4, true},
+                     {"gather4", true, true, 4, true}, {"strided_fence", false, false, 4, true}};
         for (const auto &fm : forms) {
             const std::string path = std::string(argv[1]) + "/bs_" + fm.name + ".hip";
             FILE *out = std::fopen(path.c_str(), "w");

@@ -578,3 +578,26 @@ def test_bitslice_pointer_batch_one_map(mem, knobs):
         if mem == "device":
             assert c.stats()["jit_launches"] >= 2, c.stats()
         c.close()
+
+
+def test_bitslice_xor_twin_probe(knobs):
+    """mec_set_probe(MEC_PROBE_XOR) on a wide launch runs the bit-sliced
+    kernel's arithmetic-free twin (same loads and stores): every output is
+    the XOR of the sources; off again, the code's bytes come back."""
+    knobs("MEC_BITSLICE", "2")
+    k, m, cs, n = 16, 8, 4096, 3
+    data = O.fill(n * k * cs, 8321).reshape(n, k, cs)
+    c = Codec("rs", k, m, cs)
+    par = torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)
+    c.set_probe(True)
+    c.encode(dev(data), par)
+    x = np.bitwise_xor.reduce(data, axis=1)
+    got = host(par)
+    for i in range(m):
+        assert np.array_equal(got[:, i], x), i
+    c.set_probe(False)
+    c.encode(dev(data), par)
+    want = np.stack([np.stack(O.encode("rs", k, m, [data[s, j].copy() for j in range(k)], cs)) for s in range(n)])
+    assert np.array_equal(host(par), want)
+    assert c.stats()["jit_kernels"] == 2, c.stats()
+    c.close()
