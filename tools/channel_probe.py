@@ -2,7 +2,8 @@
 """RS(10,4)@1 MiB x 4096 stripes, one arm per process, for per-channel EA
 counters: run it under
 
-  rocprofv3 -E tools/ea_channels.yaml --pmc MEC_EA_RD_CH0 ... -- python3 tools/channel_probe.py ARM
+  python3 tools/channel_probe.py --write-yaml ea_channels.yaml
+  rocprofv3 -E ea_channels.yaml --pmc MEC_EA_RD_CH0 ... -- python3 tools/channel_probe.py ARM
 
 (tools/gpu_session.sh `channels`), where the derived counters select one
 TCC instance of TCC_EA0_RDREQ / _WRREQ each, summed over the XCCs.
@@ -18,7 +19,29 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+# Derived counters per TCC instance (rocprofv3 -E): MEC_EA_<KIND>_CH<i> =
+# reduce(select(<counter>, [DIMENSION_INSTANCE=[i]]), sum), i.e. one TCC
+# channel summed over the XCCs.
+KINDS = {"RD": "TCC_EA0_RDREQ", "WR": "TCC_EA0_WRREQ", "RDLVL": "TCC_EA0_RDREQ_LEVEL",
+         "RDSTALL": "TCC_EA0_RDREQ_DRAM_CREDIT_STALL", "WRSTALL": "TCC_EA0_WRREQ_DRAM_CREDIT_STALL"}
+
+
+def write_yaml(path):
+    out = ["rocprofiler-sdk:", "  counters-schema-version: 1", "  counters:"]
+    for tag, ctr in KINDS.items():
+        for i in range(16):
+            out += [f"  - name: MEC_EA_{tag}_CH{i}",
+                    f"    description: {ctr} of TCC instance (channel) {i}, summed over the XCCs",
+                    "    properties: []", "    definitions:", "    - architectures:", "      - gfx950",
+                    f"      expression: reduce(select({ctr},[DIMENSION_INSTANCE=[{i}]]),sum)"]
+    with open(path, "w") as f:
+        f.write("\n".join(out) + "\n")
+
+
 def main():
+    if sys.argv[1] == "--write-yaml":
+        write_yaml(sys.argv[2])
+        return
     import torch
     from memec_amd import Codec, fill_random
     arm = sys.argv[1]

@@ -142,13 +142,14 @@ for step in "$@"; do
                         --output-format csv -d "$OUT/pmc_widesq_${sh}_${arm}" -o run -- python3 tools/wide_ab.py --arms $arm --shape $sh --steps 3 --warmup 1
                 done
             done ;;
-        channels)  # per-TCC-instance EA counters (CH_KINDS of tools/ea_channels.yaml) of RS(10,4)@1 MiB arms (tools/channel_probe.py), 4 a pass
+        channels)  # per-TCC-instance EA counters (CH_KINDS of tools/channel_probe.py KINDS) of RS(10,4)@1 MiB arms, 4 a pass
+            python3 tools/channel_probe.py --write-yaml "$OUT/ea_channels.yaml" || exit 1
             for arm in ${CH_ARMS:-enc_split dec_inplace dec_split}; do
                 run "ch_plain_$arm" 120 python3 tools/channel_probe.py $arm 5
                 for kind in ${CH_KINDS:-RD WR}; do
                     for q in 0 4 8 12; do
                         ctrs="MEC_EA_${kind}_CH$q MEC_EA_${kind}_CH$((q + 1)) MEC_EA_${kind}_CH$((q + 2)) MEC_EA_${kind}_CH$((q + 3))"
-                        run "ch_${arm}_${kind}_$q" 120 timeout -s KILL 100 rocprofv3 -E tools/ea_channels.yaml --pmc $ctrs \
+                        run "ch_${arm}_${kind}_$q" 120 timeout -s KILL 100 rocprofv3 -E "$OUT/ea_channels.yaml" --pmc $ctrs \
                             --output-format csv -d "$OUT/ch_${arm}_${kind}_$q" -o run -- python3 tools/channel_probe.py $arm 3
                     done
                 done
