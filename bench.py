@@ -430,6 +430,10 @@ def cpu_baseline_update(fam, k, m, cs, j, threads):
 # survivor choice, which a round trip of codewords cannot.
 REF_VS = "oracle/_ref (MemEC Coding::%s compiled from the reference sources)"
 PORT_VS = "oracle/oracle.c (restatement; oracle/_ref absent)"
+# ISA-L families: the restatement of ec_encode_data_base / the plugin's
+# decode steps, itself pinned to MemEC's USE_ISAL plugin (oracle/_ref/
+# libmemec_ref_isal.so) by the committed fixtures (tests/test_oracle.py)
+ISAL_VS = "oracle/oracle.c (ISA-L restatement, pinned to MemEC's USE_ISAL plugin by tests/golden)"
 PARITY_BYTES = 192 << 20  # stripe bytes per sampled set
 
 
@@ -465,7 +469,7 @@ def ref_encode(fam, k, m, cs, data, threads=1):
     import _oracle as O
     for s_ in range(n):
         par[s_] = np.stack(O.encode(fam, k, m, [data[s_, j].copy() for j in range(k)], cs))
-    return par, PORT_VS
+    return par, PORT_VS if fam in ("rs", "cauchy") else ISAL_VS
 
 
 def ref_decode(fam, k, m, cs, stripes, erased, threads=1):
@@ -494,7 +498,7 @@ def ref_decode(fam, k, m, cs, stripes, erased, threads=1):
         if O.decode(fam, k, m, chunks, erased, cs) != 0:
             raise RuntimeError("oracle decode failed")
         buf[s_] = np.stack(chunks)
-    return buf, PORT_VS
+    return buf, PORT_VS if fam in ("rs", "cauchy") else ISAL_VS
 
 
 def _rows(t, idx):
@@ -995,7 +999,15 @@ def main():
                   flush=True)
         return
 
-    from memec_amd import Codec, fill_random
+    from memec_amd import Codec, fill_random, set_knob
+
+    # wide codes (more than 4 outputs): compile a matrix's bit-sliced kernel
+    # at its first call, which the untimed cold step makes, instead of in
+    # the background while warmup runs the one-pass kernel (the library's
+    # default, MEC_BITSLICE=1), so the timed steps and the XOR twin run the
+    # kernel a server runs once the compile is done
+    if "MEC_BITSLICE" not in os.environ:
+        set_knob("MEC_BITSLICE", "2")
 
     # roofline.traffic measured live: PMC passes in child processes, before
     # this process touches the GPU (N = 1, plain runs, not under a profiler)
