@@ -42,6 +42,8 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "bsp2": {"MEC_BITSLICE": "3", "MEC_BS_PREFETCH": "2"}, "bsp8": {"MEC_BITSLICE": "3", "MEC_BS_PREFETCH": "8"},
         "bst4": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "4"}, "bst2": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "2"},
         "bst8": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "8"}, "bst16": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "16"},
+        "bsw4": {"MEC_BITSLICE": "3", "MEC_WPC": "4"}, "bsw6": {"MEC_BITSLICE": "3", "MEC_WPC": "6"},
+        "bsw8": {"MEC_BITSLICE": "3", "MEC_WPC": "8"}, "bsw10": {"MEC_BITSLICE": "3", "MEC_WPC": "10"},
         "bsnf": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0"}, "autonf": {"MEC_BITSLICE": "2", "MEC_BS_FENCE": "0"},
         "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"},
         # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
