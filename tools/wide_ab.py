@@ -44,6 +44,8 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "bst8": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "8"}, "bst16": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "16"},
         "bsw4": {"MEC_BITSLICE": "3", "MEC_WPC": "4"}, "bsw6": {"MEC_BITSLICE": "3", "MEC_WPC": "6"},
         "bsw8": {"MEC_BITSLICE": "3", "MEC_WPC": "8"}, "bsw10": {"MEC_BITSLICE": "3", "MEC_WPC": "10"},
+        "bsw5": {"MEC_BITSLICE": "3", "MEC_WPC": "5"}, "bsw7": {"MEC_BITSLICE": "3", "MEC_WPC": "7"},
+        "bsw12": {"MEC_BITSLICE": "3", "MEC_WPC": "12"},
         "bsnf": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0"}, "autonf": {"MEC_BITSLICE": "2", "MEC_BS_FENCE": "0"},
         "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"},
         # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
