@@ -346,6 +346,7 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
                 L.rows = int(ds.size());
                 L.len = c->cs;
                 L.n_stripes = n;
+                L.vand = coef_vand(cf, ds.size(), M.K);
                 for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
                 for (size_t r = 0; r < ds.size(); ++r) L.dst_off[r] = ds[r];
                 return jit_launch(c, jk, L, st);

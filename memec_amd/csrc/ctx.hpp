@@ -345,6 +345,7 @@ void mg_release(mec_ctx *c);
 // kernel.  jit_kernel: the kernel for this matrix, or nullptr (compiling,
 // failed, capped, MEC_BITSLICE=0) — the caller then runs gf8_mg_kernel.
 bool jit_wanted(const mec_ctx *c, size_t nd, size_t ns, const Mat &coef, bool gathered);
+bool coef_vand(const Mat &coef, size_t nd, size_t ns);
 JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool accumulate, bool gather,
                       bool twin = false);
 int jit_launch(mec_ctx *c, JitKernel *k, const BsLaunch &L, hipStream_t stream);

@@ -108,31 +108,31 @@ uint64_t env_u64(const char *name, uint64_t dflt) {
 }  // namespace
 
 // Which wide launches take the bit-sliced kernel (MEC_BITSLICE unset, 1 or
-// 2): matrices with at least half as many sources as outputs that are
-// dense (decodes, ISA-L Cauchy), have 12+ sources, or are coded through
-// pointer rows (one-map batches).  Strided launches below 12 sources keep
-// gf8_mg_kernel for Vandermonde-structured matrices (row 0 and column 0 all
-// ones: Jerasure / ISA-L RS encodes), whose plain-XOR row and column make it
-// cheaper there: RS(10,6)@256 KiB encode 77.7 % against 70.5, RS(8,5)@16
-// KiB 80.1 against 71.4 — but through pointer rows the gathered one-pass
-// kernel loses that lead (RS(10,6) batch 71.7 against 79.1).  With fewer
-// than half as many sources as outputs the bit-sliced kernel's per-output
-// work dominates: RS(4,12)@1 MiB encode 61 against 79, ISA-L Cauchy(4,12)
-// 63 against 75 (its in-place RS(4,12) decode of 12 is the exception, 81
-// against 75).  Elsewhere +4-24 points: RS(16,8) 72.8 against 68.8, ISA-L
-// RS(12,8) 77.5 against 68.8, 8-erasure decode 77.0 against 56.9
-// (tools/wide_ab.py, profiles/r05/wide_ab_*.jsonl).  MEC_BITSLICE=3 takes it
-// for every wide launch (A/B), 0 never.
+// 2): every byte-wise launch of more than 4 outputs on chunks that are a
+// multiple of 16 bytes.  With the wave caps of plan_bs it leads the
+// one-pass kernel on every wide shape measured, the Vandermonde encodes
+// under 12 sources included (RS(10,6)@256 KiB encode 78.9-79.9 % against
+// 74.7-77.7, RS(8,5)@16 KiB 82.8-83.4 against 76.3-80.1, RS(4,12)@1 MiB
+// 81.8 against 77.7-78.8; ISA-L Cauchy(4,12) ties, 75-76 both), and by
+// 7-24 points on the rest (tools/wide_ab.py, profiles/r05/wide_*.jsonl).
+// The one-pass kernel serves the rest: a matrix whose kernel is still
+// compiling, other chunk sizes, MEC_BITSLICE=0.  MEC_BITSLICE=3 also
+// compiles synchronously, like 2 (A/B).
 bool jit_wanted(const mec_ctx *c, size_t nd, size_t ns, const Mat &coef, bool gathered) {
+    (void)ns;
+    (void)coef;
+    (void)gathered;
     const int64_t kn = detail::knob(detail::kKnobBitslice);
-    if (kn == 0 || !c->byte_wise() || nd <= size_t(kMaxRows) || c->cs % 16 != 0) return false;
-    if (kn == 3) return true;
-    if (nd > 2 * ns) return false;
-    if (gathered || ns >= 12) return true;
+    return kn != 0 && c->byte_wise() && nd > size_t(kMaxRows) && c->cs % 16 == 0;
+}
+
+// Row 0 and column 0 all ones: a Vandermonde-structured encode (Jerasure's
+// distribution rows, ISA-L gf_gen_rs_matrix), which takes its own wave cap.
+bool coef_vand(const Mat &coef, size_t nd, size_t ns) {
     bool vand = true;
     for (size_t j = 0; j < ns && vand; ++j) vand = coef[j] == 1;
     for (size_t r = 0; r < nd && vand; ++r) vand = coef[r * ns] == 1;
-    return !vand;
+    return vand;
 }
 
 // The kernel for (coef, accumulate, addressing), compiling it if needed;

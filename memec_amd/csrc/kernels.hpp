@@ -164,6 +164,7 @@ struct BsLaunch {
     uint64_t len;
     uint32_t n_stripes;
     uint32_t tpb;  // gathered: 2 KiB tiles per block the kernel was built for (0 = MEC_BS_TPB / rule)
+    bool vand;     // row 0 and column 0 all ones (the Vandermonde-structured encodes): the wave cap (plan_bs)
 };
 
 hipError_t launch_gf8(const Gf8Launch &L, hipStream_t stream);

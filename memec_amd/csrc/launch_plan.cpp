@@ -384,6 +384,26 @@ KernelPlan plan_bm_gather(const GatherLaunch &L, uint32_t s0) {
     return p;
 }
 
+uint32_t bs_target_waves(bool in_place, bool vand) {
+    // A strided bit-sliced wave streams 2 KiB of every one of its 13-28
+    // chunks (32-56 KiB), 4 sources ahead; uncapped, the VGPR budget puts 12
+    // such waves on a CU and the memory side queues them into lower
+    // throughput (RS(16,8)@64 KiB encode 71.6-73.8 % of 8 TB/s).  Capped
+    // (tools/wide_ab.py bsw<n> arms, three rounds on two boxes,
+    // profiles/r05/wide_cap_box8.jsonl, wide_cap_box9.jsonl): split
+    // Vandermonde encodes run best at 5 waves per CU (RS(16,8) 79.6-80.1,
+    // RS(10,6)@256 KiB 78.9-79.9, RS(8,5)@16 KiB 82.8-83.4, RS(4,12)@1 MiB
+    // 81.8, ISA-L RS(12,8) 80.1-80.7), split dense ones at 6 (ISA-L
+    // Cauchy(12,6) 80.6-80.7, 69 at 5; Cauchy(20,8)@4 KiB 69.2-69.9 and
+    // (4,12) 75.2-76.2 would take 5 but the cliff of (12,6) rules it out),
+    // in-place decodes at 8 (RS(10,6) 78.7 against 74.5 uncapped and 58 at
+    // 4-5; RS(16,8) 77.9-78.2 against 77.1).  Gathered launches stay
+    // uncapped: a cap costs them 10-37 points (their blocks first wait on
+    // the pointer row).  MEC_WPC overrides.
+    if (in_place) return 8;
+    return vand ? 5 : 6;
+}
+
 uint32_t bs_gather_tpb() {
     const int64_t kt = knob(kKnobBsTpb);
     return kt != kKnobUnset && kt > 0 ? uint32_t(kt) : 1u;
@@ -414,9 +434,7 @@ KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
         const uint8_t *dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
         p.win = launch_windows(src, int64_t(p.ns) * L.src_stripe_stride, dst, int64_t(p.ns) * L.dst_stripe_stride);
     }
-    // occupancy is the program's VGPRs (~190 for 16 sources x 8 rows); only
-    // a forced MEC_WPC caps it
-    p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0, 0);
+    p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0, L.stab ? 0u : bs_target_waves(p.win > 1, L.vand));
     common_ok(p, uint64_t(p.geo.tiles) * p.tpb * 2048);
     return p;
 }

@@ -161,6 +161,7 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
             L.rows = int(nd);
             L.len = c->cs;
             L.n_stripes = n_stripes;
+            L.vand = coef_vand(coef, nd, ns);
             for (size_t j = 0; j < ns; ++j) L.src_off[j] = lay.src_off[j];
             for (size_t r = 0; r < nd; ++r) L.dst_off[r] = lay.dst_off[r];
             return jit_launch(c, jk, L, stream);

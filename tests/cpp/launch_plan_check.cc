@@ -161,8 +161,9 @@ static void check_mg(int k, int rows, uint64_t chunk, uint32_t n, bool in_place,
     }
 }
 
-static void check_bs(int k, int rows, uint64_t chunk, uint32_t n, bool in_place, bool gather) {
+static void check_bs(int k, int rows, uint64_t chunk, uint32_t n, bool in_place, bool gather, bool vand) {
     BsLaunch L{};
+    L.vand = vand;
     const Layout ly = layout(in_place, chunk, k, rows);
     L.src = ly.src;
     L.dst = ly.dst;
@@ -183,6 +184,9 @@ static void check_bs(int k, int rows, uint64_t chunk, uint32_t n, bool in_place,
         common(p, uint64_t(p.geo.tiles) * p.tpb * 2048);
         if (!p.ok || p.ns == 0) break;
         if (p.bt != uint32_t(kWaveBlock)) bad("bit-sliced kernels are one-wave blocks", p);
+        if (gather && p.lds_dynamic != 0 && knob(kKnobWpc) == kKnobUnset) bad("gathered bit-sliced launches are uncapped", p);
+        if (!gather && knob(kKnobWpc) == kKnobUnset && p.lds_dynamic * bs_target_waves(p.win > 1, vand) > kLdsPerCu)
+            bad("bit-sliced wave cap reserves more than a CU's LDS", p);
         if (p.tpb < 1 || uint64_t(p.geo.tiles) * p.tpb * 2048 < chunk) bad("tiles do not cover the chunk", p);
         if (uint64_t(p.geo.tiles - 1) * p.tpb * 2048 >= chunk) bad("a block with no tile", p);
         covered += p.ns;
@@ -271,7 +275,7 @@ static void sweep() {
                         }
                         if (chunk % 16 == 0)
                             for (int rows = kMaxRows + 1; k + rows <= kMaxSrc; ++rows) {
-                                if (vand) check_bs(k, rows, chunk, n, ip, rows % 2 == 0);
+                                check_bs(k, rows, chunk, n, ip, (rows + int(vand)) % 2 == 0, vand);
                                 check_mg(k, rows, chunk, n, ip, vand, false, false);
                                 check_mg(k, rows, chunk, n, ip, vand, true, false);
                                 check_mg(k, rows, chunk, n, ip, vand, false, true);

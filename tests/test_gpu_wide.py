@@ -127,6 +127,7 @@ def test_wide_group_rows_forced(fam, rows, knobs):
     """8 outputs coded in groups of 3, 4 or 8 rows (MEC_MG_ROWS; the rule
     picks 8 for RS(16,8) and the dense ISA-L Cauchy(12,8)): same bytes,
     encode and in-place decode of 8 erasures, plus an accumulating update."""
+    knobs("MEC_BITSLICE", "0")  # the one-pass kernel itself (the bit-sliced one takes these once compiled)
     knobs("MEC_MG_ROWS", rows)
     for k, m, cs, n in [(16, 8, 4096, 3), (12, 8, 2048, 3), (20, 8, 1024, 2), (24, 8, 1024, 2), (12, 16, 512, 2)]:
         data = O.fill(n * k * cs, 60 + k + m).reshape(n, k, cs)
@@ -161,6 +162,7 @@ def test_forced_three_row_groups_31_rows(fam, knobs):
     back to the rule (8 groups of 4) here; encode, a 30-erasure in-place
     decode and an accumulating update equal the oracle, and RS(1,30) keeps
     the forced 10 x 3 groups."""
+    knobs("MEC_BITSLICE", "0")
     knobs("MEC_MG_ROWS", "3")
     for k, m in [(1, 31), (1, 30), (2, 30)]:
         cs, n = 512, 3
@@ -188,7 +190,7 @@ def test_forced_three_row_groups_31_rows(fam, knobs):
         c.close()
 
 
-def test_one_pass_table_cache_is_bounded(monkeypatch):
+def test_one_pass_table_cache_is_bounded(monkeypatch, knobs):
     """The one-pass kernel's permute tables are cached per matrix up to
     MEC_MG_CACHE_BYTES (the cache grew without bound, one
     device allocation per erasure pattern).  RS(16,8) decodes of 60
@@ -197,6 +199,7 @@ def test_one_pass_table_cache_is_bounded(monkeypatch):
     4-row launches, and no device memory leaks past the cap."""
     k, m, cs, n = 16, 8, 1024, 2
     monkeypatch.setenv("MEC_MG_CACHE_BYTES", str(3 * 8 * 16 * 32))
+    knobs("MEC_BITSLICE", "0")
     c = Codec("rs", k, m, cs)
     data = O.fill(n * k * cs, 321).reshape(n, k, cs)
     st = torch.zeros(n, k + m, cs, dtype=torch.uint8, device=DEV)
@@ -459,14 +462,14 @@ def test_bitslice_encode_decode_update_vs_oracle(fam, knobs):
 
 
 def test_bitslice_rule(knobs):
-    """MEC_BITSLICE=2: the rule (jit.cpp jit_wanted) — Vandermonde-structured
-    encodes under 12 sources stay on gf8_mg_kernel when strided, from 12 up,
-    every dense matrix (a decode) and every one-map pointer batch take the
-    bit-sliced kernel, unless the outputs outnumber twice the sources
-    (RS(4,12)); same bytes."""
+    """MEC_BITSLICE=2: the rule (jit.cpp jit_wanted) — every byte-wise launch
+    of more than 4 outputs on 16-byte-multiple chunks takes the bit-sliced
+    kernel: Vandermonde encodes under 12 sources and outputs outnumbering
+    the sources included (their wave caps, plan_bs), strided and through
+    pointer rows; 4-output launches do not; same bytes."""
     knobs("MEC_BITSLICE", "2")
-    for k, m, cs, want_enc, want_dec in [(10, 6, 2048, False, True), (12, 6, 2048, True, True),
-                                         (4, 12, 2048, False, False)]:
+    for k, m, cs, want_enc, want_dec in [(10, 6, 2048, True, True), (12, 6, 2048, True, True),
+                                         (4, 12, 2048, True, True), (10, 4, 2048, False, False)]:
         n = 2
         data = O.fill(n * k * cs, 9100 + k).reshape(n, k, cs)
         want = np.stack([np.stack(O.encode("rs", k, m, [data[s, j].copy() for j in range(k)], cs)) for s in range(n)])
@@ -485,15 +488,14 @@ def test_bitslice_rule(knobs):
         torch.cuda.synchronize()
         assert torch.equal(t, st)
         assert c.stats()["jit_launches"] == before + int(want_dec), c.stats()
-        # through pointer rows (a one-map batch) Vandermonde matrices under
-        # 12 sources take it too, unless outputs exceed twice the sources
+        # through pointer rows (a one-map batch) too
         par2 = torch.zeros_like(par)
         before = c.stats()["jit_launches"]
         c.encode_batch([data_t[s, j].data_ptr() for s in range(n) for j in range(k)],
                        [par2[s, i].data_ptr() for s in range(n) for i in range(m)], mem="device")
         torch.cuda.synchronize()
         assert torch.equal(par2, par)
-        assert c.stats()["jit_launches"] == before + int(m <= 2 * k), (k, m, c.stats())
+        assert c.stats()["jit_launches"] == before + int(m > 4), (k, m, c.stats())
         c.close()
 
 
