@@ -99,6 +99,7 @@ def run(arms_list, steps, warmup, shapes):
             for kn in KNOBS:  # every knob any arm sets: unset unless this arm sets it
                 memec_amd.set_knob(kn, ARMS[arm].get(kn))
             c.set_probe(ARMS[arm].get("PROBE") == "xor")
+            j0 = c.stats()["jit_launches"]
             for _ in range(warmup):
                 step()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -111,6 +112,7 @@ def run(arms_list, steps, warmup, shapes):
             arms[arm] = {"ms_per_step": round(ms, 4), "GBps": round(alg / (ms * 1e-3) / 1e9, 1),
                          "frac": round(alg / (ms * 1e-3) / 8e12, 4)}
             arms[arm]["digest"] = int(result().view(torch.int64).sum().item())
+            arms[arm]["jit_launches"] = c.stats()["jit_launches"] - j0  # warmup + timed steps on the JIT kernel
         for kn in KNOBS:
             memec_amd.set_knob(kn, None)
         c.set_probe(False)
