@@ -45,6 +45,13 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "bsw4": {"MEC_BITSLICE": "3", "MEC_WPC": "4"}, "bsw6": {"MEC_BITSLICE": "3", "MEC_WPC": "6"},
         "bsw8": {"MEC_BITSLICE": "3", "MEC_WPC": "8"}, "bsw10": {"MEC_BITSLICE": "3", "MEC_WPC": "10"},
         "bsnocap": {"MEC_BITSLICE": "3", "MEC_WPC": "0"}, "mgw": {"MEC_BITSLICE": "0"},
+        # gathered: tiles per block x wave cap
+        "t2w8": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "2", "MEC_WPC": "8"},
+        "t2w12": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "2", "MEC_WPC": "12"},
+        "t4w8": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "4", "MEC_WPC": "8"},
+        "t4w12": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "4", "MEC_WPC": "12"},
+        "t8w8": {"MEC_BITSLICE": "3", "MEC_BS_TPB": "8", "MEC_WPC": "8"},
+        "t1w12": {"MEC_BITSLICE": "3", "MEC_WPC": "12"}, "t1w16": {"MEC_BITSLICE": "3", "MEC_WPC": "16"},
         "bsw5": {"MEC_BITSLICE": "3", "MEC_WPC": "5"}, "bsw7": {"MEC_BITSLICE": "3", "MEC_WPC": "7"},
         "bsw12": {"MEC_BITSLICE": "3", "MEC_WPC": "12"},
         "bsnf": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0"}, "autonf": {"MEC_BITSLICE": "2", "MEC_BS_FENCE": "0"},
