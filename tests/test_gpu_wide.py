@@ -603,3 +603,36 @@ def test_bitslice_xor_twin_probe(knobs):
     assert np.array_equal(host(par), want)
     assert c.stats()["jit_kernels"] == 2, c.stats()
     c.close()
+
+
+@pytest.mark.parametrize("m", list(range(5, 32)))
+def test_bitslice_every_output_count(m, knobs):
+    """The bit-sliced kernel of every output count m = 5..31 (sync compile,
+    MEC_BITSLICE=2) at one, half and all of the source counts k + m <= 32
+    allows: the RS encode (Vandermonde, capped split launch) and an in-place
+    decode of min(m, 8) erasures over random non-codewords (dense matrix,
+    capped in-place launch), on a chunk with a partial 2 KiB tile (2064 B),
+    equal to the oracle."""
+    knobs("MEC_BITSLICE", "2")
+    cs, n = 2064, 2
+    for k in sorted({1, max(1, (32 - m) // 2), 32 - m}):
+        data = O.fill(n * k * cs, 7700 + 31 * m + k).reshape(n, k, cs)
+        want = np.stack([np.stack(O.encode("rs", k, m, [data[s, j].copy() for j in range(k)], cs)) for s in range(n)])
+        c = Codec("rs", k, m, cs)
+        par = torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)
+        c.encode(dev(data), par)
+        assert np.array_equal(host(par), want), (k, m)
+        base = O.fill(n * (k + m) * cs, 7800 + 31 * m + k).reshape(n, k + m, cs)
+        rng = np.random.default_rng(31 * m + k)
+        pat = sorted(rng.choice(k + m, size=min(m, 8), replace=False).tolist())
+        t = dev(base.copy())
+        c.decode(t, sum(1 << i for i in range(k + m) if i not in pat))
+        got = host(t)
+        for s in range(n):
+            chunks = [base[s, i].copy() for i in range(k + m)]
+            assert O.decode("rs", k, m, chunks, pat, cs) == 0
+            for i in pat:
+                assert np.array_equal(got[s, i], chunks[i]), (k, m, pat, s, i)
+        st = c.stats()
+        assert st["jit_failed"] == 0 and st["jit_launches"] >= 1 + int(len(pat) > 4), (k, m, st)
+        c.close()
