@@ -22,7 +22,12 @@ pids=()
 for f in memec_amd/csrc/*.hip memec_amd/csrc/*.cpp; do
     o="$OUT/$(basename "${f%.*}").o"
     objs+=("$o")
-    if [ ! -f "$o" ] || [ "$f" -nt "$o" ]; then
+    # rebuilt when the source or any header is newer (a unit compiled
+    # against an older ctx.hpp would disagree on mec_ctx's layout)
+    stale=0
+    [ ! -f "$o" ] || [ "$f" -nt "$o" ] && stale=1
+    for h in memec_amd/csrc/*.hpp include/mec.h; do [ "$h" -nt "$o" ] && stale=1; done
+    if [ $stale = 1 ]; then
         $HIPCC $FLAGS -c -o "$o" "$f" &
         pids+=($!)
         if [ ${#pids[@]} -ge 8 ]; then wait "${pids[0]}"; pids=("${pids[@]:1}"); fi
