@@ -200,10 +200,11 @@ void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out) 
     }
 }
 
-std::string bs_source(const BsProgram &p, bool gather, int waves, int prefetch, bool loop, bool fence) {
+std::string bs_source(const BsProgram &p, bool gather, int waves, int prefetch, bool loop, bool fence, bool vrow) {
     std::string s;
     s.reserve(p.ops.size() * 48 + 4096);
     s += gather ? "#define MEC_GATHER 1\n" : "#define MEC_GATHER 0\n";
+    s += gather && vrow ? "#define MEC_VROW 1\n" : "#define MEC_VROW 0\n";
     if (waves > 0) s += "#define MEC_WAVES __attribute__((amdgpu_waves_per_eu(" + std::to_string(waves) + ")))\n";
     else s += "#define MEC_WAVES\n";
     s += R"HIP(
@@ -217,7 +218,7 @@ struct BsParams {
     i64 sss, dss;
     const u64 *stab, *dtab;
     u32 sstride, dstride;
-    u32 chunk, tiles, nstr, win, s0, tpb;
+    u32 chunk, tiles, xcd, win, s0, tpb;
     i64 src_off[32];
     i64 dst_off[32];
 };
@@ -239,20 +240,41 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
     if (!MEC_GATHER && p.win > 1) {  // in-place layouts: windows taken round-robin (stream_common.hpp block_order)
         const u32 per = gridDim.x / p.win;
         if (bid < per * p.win) bid = (bid % p.win) * per + bid / p.win;
+    } else if (p.xcd) {  // blocks dealt round-robin over the 8 XCDs: each XCD one contiguous run (plan_bs)
+        const u32 per = gridDim.x >> 3;
+        if (bid < per * 8u) bid = (bid & 7u) * per + (bid >> 3);
     }
     // block b of a stripe codes tiles [b * tpb, (b + 1) * tpb): its chunk
     // addresses (pointer-row loads when gathered) are read once
     const u32 stripe = bid / p.tiles, tile0 = (bid - stripe * p.tiles) * p.tpb;
     if (tile0 * 2048u >= p.chunk) return;
     const u64 gs = (u64)p.s0 + stripe;
-#if MEC_GATHER
+#if MEC_GATHER && !MEC_VROW
     auto src_at = [&](int j) -> u64 { return mec_uniform64(p.stab[gs * p.sstride + p.src_off[j]]); };
     auto dst_at = [&](int r) -> u64 { return mec_uniform64(p.dtab[gs * p.dstride + p.dst_off[r]]); };
-#else
+#elif !MEC_GATHER
     auto src_at = [&](int j) -> u64 { return (u64)(p.src + (i64)stripe * p.sss + p.src_off[j]); };
     auto dst_at = [&](int r) -> u64 { return (u64)(p.dst + (i64)stripe * p.dss + p.dst_off[r]); };
 #endif
 )HIP";
+    if (gather && vrow) {
+        // the block's pointer row in one vector load: lane j < 32 fetches
+        // source j's entry, lane 32 + r output r's; each use reads its lane
+        // back into SGPRs (v_readlane), so no source waits on a scalar load
+        s += "    i64 mo = -1;\n";
+        for (int j = 0; j < p.ns; ++j)
+            s += "    mo = threadIdx.x == " + std::to_string(j) + "u ? p.src_off[" + std::to_string(j) + "] : mo;\n";
+        for (int r = 0; r < p.nd; ++r)
+            s += "    mo = threadIdx.x == " + std::to_string(32 + r) + "u ? p.dst_off[" + std::to_string(r) + "] : mo;\n";
+        s += "    const u64 *mrow = threadIdx.x < 32u ? p.stab + gs * p.sstride : p.dtab + gs * p.dstride;\n"
+             "    const u64 mptr = mo >= 0 ? mrow[mo] : 0ull;\n"
+             "    auto lane64 = [&](int l) -> u64 {\n"
+             "        return ((u64)(u32)__builtin_amdgcn_readlane((int)(u32)(mptr >> 32), l) << 32) |\n"
+             "               (u32)__builtin_amdgcn_readlane((int)(u32)mptr, l);\n"
+             "    };\n"
+             "    auto src_at = [&](int j) -> u64 { return lane64(j); };\n"
+             "    auto dst_at = [&](int r) -> u64 { return lane64(32 + r); };\n";
+    }
     char buf[320];
     // source units: the first `depth` sources' loads up front, then each
     // further source's loads just before the combine of the source `depth`
@@ -304,9 +326,9 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
         s += buf;
         ++nfence;
     };
-    // (gathered: the pointer-row entry is re-read per tile, from the scalar
-    // cache after the block's first tile; holding all K + R pointers across
-    // the tile loop spilled SGPRs)
+    // (gathered: with vrow each use reads its entry back from the row's
+    // lane (two VGPRs held across a tile loop); without, the entry is
+    // re-read per use, from the scalar cache after the first)
     for (int j = 0; j < p.ns; ++j) {
         std::snprintf(buf, sizeof buf, "#define sp%d src_at(%d)\n", j, j);
         s += buf;
@@ -316,15 +338,18 @@ extern "C" __global__ __launch_bounds__(64) MEC_WAVES void mec_bs(const BsParams
         s += buf;
     }
     // looped gathered kernels walk the block's tiles; the others take one
-    // tile per block (straight-line: the loop costs registers)
+    // tile per block (straight-line: the loop costs registers).  With vrow no
+    // lane leaves before the row's last v_readlane: lanes past the chunk's
+    // end run on, their loads reading zeros and their stores dropped by the
+    // buffer resource's bounds (num_records = chunk)
+    const char *past = gather && vrow ? "" : loop ? "    if (off >= p.chunk) break;\n" : "    if (off >= p.chunk) return;\n";
     if (gather && loop)
-        s += "    for (u32 t = 0; t < p.tpb; ++t) {\n"
-             "    const u32 off = (tile0 + t) * 2048u + threadIdx.x * 16u;\n"
-             "    if (off >= p.chunk) break;\n";
+        s += std::string("    for (u32 t = 0; t < p.tpb; ++t) {\n"
+                         "    if ((tile0 + t) * 2048u >= p.chunk) break;\n"
+                         "    const u32 off = (tile0 + t) * 2048u + threadIdx.x * 16u;\n") + past;
     else
-        s += "    {\n"
-             "    const u32 off = tile0 * 2048u + threadIdx.x * 16u;\n"
-             "    if (off >= p.chunk) return;\n";
+        s += std::string("    {\n"
+                         "    const u32 off = tile0 * 2048u + threadIdx.x * 16u;\n") + past;
     for (int j = 0; j < depth; ++j) emit_load(j);
     int next_load = depth;
     for (int r = 0; r < p.nd; ++r) {

@@ -81,8 +81,11 @@ void bs_run(const BsProgram &p, const uint8_t *const *src, uint8_t *const *out);
 // loaded units, so the compiler cannot start a source's transposes and
 // combinations before the previous source's are consumed (one source's
 // combinations live at a time).
+// vrow (gathered): the block's whole pointer row arrives in one vector load
+// (one lane per entry, read back with v_readlane at each use); otherwise
+// each entry is a scalar load at its use, and the compiler waits on each.
 std::string bs_source(const BsProgram &p, bool gather, int waves = 0, int prefetch = 0, bool loop = false,
-                      bool fence = false);
+                      bool fence = false, bool vrow = false);
 
 // Kernel arguments of every generated kernel (the same layout in the
 // generated source, bs_source).  Strided: source j of stripe s at src + s *
@@ -94,7 +97,7 @@ struct BsParams {
     int64_t sss, dss;
     const uint64_t *stab, *dtab;
     uint32_t sstride, dstride;
-    uint32_t chunk, tiles, nstr, win, s0, tpb;  // tiles = blocks per stripe, each tpb 2 KiB tiles
+    uint32_t chunk, tiles, xcd, win, s0, tpb;  // tiles = blocks per stripe, each tpb 2 KiB tiles; xcd: XCD runs
     int64_t src_off[32];
     int64_t dst_off[32];
 };

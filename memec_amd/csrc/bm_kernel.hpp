@@ -84,31 +84,36 @@ __global__ __launch_bounds__(BT) void bm_kernel(const BmParams<W, R> p) {
     const uint32_t bid = block_order(p.win);
     uint32_t stripe, tile;
     stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, p.skew, stripe, tile);
-    const uint32_t u = tile * BT + threadIdx.x;
-    if (u >= p.units) return;
+    uint32_t u = tile * BT + threadIdx.x;
+    if constexpr (G) {
+        if (!gather_unit<BT>(tile, p.units, u)) return;
+    } else if (u >= p.units) {
+        return;
+    }
     vec acc[ROWS];
     vec d[W], nx[W];
     if constexpr (G) {
         const uint32_t off = u * (4 * VW);
         const uint32_t pk = uint32_t(p.packet);
         const uint64_t s = p.s0 + stripe;
-        const uint64_t *srow = p.stab + s * p.sstride;
-        const uint64_t *drow = p.dtab + s * p.dstride;
+        // the stripe's pointer row, one vector load (stream_common.hpp row_fetch)
+        static_assert(R <= 32, "pointer row lanes");
+        const uint64_t row = row_fetch(p.stab + s * p.sstride, p.src_off, p.k, p.dtab + s * p.dstride, p.dst_off, R);
         __amdgpu_buffer_rsrc_t dr[R];
 #pragma unroll
-        for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(drow[p.dst_off[i]], p.chunk);
+        for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(row_entry(row, 32u + i), p.chunk);
 #pragma unroll
         for (int i = 0; i < R; ++i)
 #pragma unroll
             for (int l = 0; l < W; ++l) acc[i * W + l] = p.accumulate ? buf_ld<vec>(dr[i], off + l * pk, true) : vec(0);
         {
-            const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(srow[p.src_off[0]], p.chunk);
+            const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(row_entry(row, 0), p.chunk);
 #pragma unroll
             for (int x = 0; x < W; ++x) d[x] = buf_ld<vec>(sr, off + x * pk, true);
         }
         for (uint32_t j = 0; j < p.k; ++j) {
             if (j + 1 < p.k) {
-                const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(srow[p.src_off[j + 1]], p.chunk);
+                const __amdgpu_buffer_rsrc_t sr = chunk_rsrc(row_entry(row, j + 1), p.chunk);
 #pragma unroll
                 for (int x = 0; x < W; ++x) nx[x] = buf_ld<vec>(sr, off + x * pk, true);
             }

@@ -158,8 +158,12 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     const uint32_t bid = block_order(p.win);
     uint32_t stripe, tile;
     stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, p.skew, stripe, tile);
-    const uint32_t u = tile * BT + threadIdx.x;
-    if (u >= p.units) return;
+    uint32_t u = tile * BT + threadIdx.x;
+    if constexpr (G) {
+        if (!gather_unit<BT>(tile, p.units, u)) return;
+    } else if (u >= p.units) {
+        return;
+    }
     // Every chunk is a buffer resource (SGPR base, 32-bit lane offsets) in
     // both modes: strided chunk bases are uniform per block too, and the
     // same non-temporal stream runs 2-3 points faster through buffer
@@ -168,12 +172,14 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     const uint32_t off = u * 16;
     // chunk addresses (uniform): source j / output i of this stripe
     const uint64_t gs = p.s0 + stripe;
+    static_assert(K <= 32 && R <= 32, "pointer row lanes (row_fetch)");
+    const uint64_t row = G ? row_fetch(p.stab + gs * p.sstride, p.src_off, K, p.dtab + gs * p.dstride, p.dst_off, R) : 0;
     auto src_at = [&](int j) -> uint64_t {
-        if constexpr (G) return p.stab[gs * p.sstride + p.src_off[j]];
+        if constexpr (G) return row_entry(row, uint32_t(j));
         else return uint64_t(uintptr_t(p.src + int64_t(stripe) * p.sss + p.src_off[j]));
     };
     auto dst_at = [&](int i) -> uint64_t {
-        if constexpr (G) return p.dtab[gs * p.dstride + p.dst_off[i]];
+        if constexpr (G) return row_entry(row, 32u + uint32_t(i));
         else return uint64_t(uintptr_t(p.dst + int64_t(stripe) * p.dss + p.dst_off[i]));
     };
     u32x4 d[K];
@@ -231,15 +237,22 @@ __global__ __launch_bounds__(kWaveBlock) void gf8_mg_kernel(const Gf8MgParams<K>
     const uint32_t bid = block_order(p.win);
     uint32_t stripe, tile;
     stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, p.skew, stripe, tile);
-    const uint32_t u = tile * kWaveBlock + threadIdx.x;
-    if (u >= p.units) return;
+    uint32_t u = tile * kWaveBlock + threadIdx.x;
+    if constexpr (G) {
+        if (!gather_unit<kWaveBlock>(tile, p.units, u)) return;
+    } else if (u >= p.units) {
+        return;
+    }
     const uint32_t off = u * 16;
     const uint64_t gs = p.s0 + stripe;
+    static_assert(K <= 32, "pointer row lanes (row_fetch)");
+    const uint64_t row =
+        G ? row_fetch(p.stab + gs * p.sstride, p.src_off, K, p.dtab + gs * p.dstride, p.dst_off, p.groups * R) : 0;
     u32x4 d[K];
 #pragma unroll
     for (int j = 0; j < K; ++j) {
         MEC_DASSERT(!G || (p.src_off[j] >= 0 && p.src_off[j] < int64_t(p.sstride)));
-        const uint64_t a = G ? uniform64(p.stab[gs * p.sstride + p.src_off[j]])
+        const uint64_t a = G ? row_entry(row, uint32_t(j))
                              : uint64_t(uintptr_t(p.src + int64_t(stripe) * p.sss + p.src_off[j]));
         d[j] = buf_ld<u32x4>(chunk_rsrc(a, p.chunk), off, true);
     }
@@ -251,7 +264,7 @@ __global__ __launch_bounds__(kWaveBlock) void gf8_mg_kernel(const Gf8MgParams<K>
             MEC_DASSERT(g * R + i < uint32_t(kMaxSrc));
             MEC_DASSERT(!G || p.dst_off[g * R + i] < int64_t(p.dstride));
             const int64_t o = p.dst_off[g * R + i];
-            const uint64_t a = o < 0 ? 0 : G ? uniform64(p.dtab[gs * p.dstride + uint64_t(o)]) : uint64_t(uintptr_t(db + o));
+            const uint64_t a = o < 0 ? 0 : G ? row_entry(row, 32u + g * R + uint32_t(i)) : uint64_t(uintptr_t(db + o));
             dr[i] = chunk_rsrc(a, p.chunk);
         }
         u32x4 acc[R];

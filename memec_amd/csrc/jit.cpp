@@ -168,6 +168,10 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     const bool fence = fk == detail::kKnobUnset ? gather : fk != 0;
     key += char(fence ? 1 : 0);
     key += char(twin ? 1 : 0);
+    // gathered: the pointer row in one vector load (bitslice.hpp vrow)
+    const int64_t vk = detail::knob(detail::kKnobBsVrow);
+    const bool vrow = vk == detail::kKnobUnset || vk != 0;
+    key += char(vrow ? 1 : 0);
     JitCache &J = c->jit;
     const bool sync = detail::knob(detail::kKnobBitslice) >= 2;
     std::shared_ptr<JitKernel> k;
@@ -188,7 +192,7 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     }
     if (fresh) {
         auto src = std::make_shared<std::string>(bs_source(twin ? bs_build_twin(int(nd), int(ns), accumulate) : bs_build(coef.data(), int(nd), int(ns), accumulate),
-                      gather, waves, prefetch, loop, fence));
+                      gather, waves, prefetch, loop, fence, vrow));
         const int device = c->device;
         auto done = [&J, k] {
             std::lock_guard<std::mutex> g(J.mu);
@@ -235,7 +239,7 @@ int jit_launch(mec_ctx *c, JitKernel *k, const BsLaunch &L0, hipStream_t stream)
         if (!pl.ok) return fail(MEC_EINVAL, "bit-sliced launch: %s", pl.why);
         p.tiles = pl.geo.tiles;
         p.tpb = pl.tpb;
-        p.nstr = pl.ns;
+        p.xcd = pl.xcd;
         p.win = pl.win;
         p.s0 = s0;
         if (!L.stab) {

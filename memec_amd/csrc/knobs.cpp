@@ -32,6 +32,8 @@ constexpr KnobSpec kSpecs[] = {
     {"MEC_BS_TPB", kKnobBsTpb, 0, 64, {}, 0},
     {"MEC_TILE_SKEW", kKnobTileSkew, 0, 1024, {}, 0, 8},
     {"MEC_BS_FENCE", kKnobBsFence, 0, 1, {}, 0, 0},
+    {"MEC_BS_XCD", kKnobBsXcd, 0, 1, {}, 0, 0},
+    {"MEC_BS_VROW", kKnobBsVrow, 0, 1, {}, 0, 0},
 };
 // every knob but MEC_SGROUP's run half has its own variable
 static_assert(sizeof(kSpecs) / sizeof(kSpecs[0]) == kKnobCount - 1, "a knob whose variable is never read");

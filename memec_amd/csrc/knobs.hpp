@@ -38,6 +38,8 @@ enum Knob : int {
     kKnobBsTpb,       // MEC_BS_TPB=<n>: 2 KiB tiles per block of the gathered ones (0 = rule: 1, straight-line)
     kKnobTileSkew,    // MEC_TILE_SKEW=<tiles>: strided identity-map launches rotate stripe s's tiles by s * n (0 = none; unset = rule)
     kKnobBsFence,     // MEC_BS_FENCE=0|1: bit-sliced kernels compiled with scheduling fences between sources (unset: gathered ones)
+    kKnobBsXcd,       // MEC_BS_XCD=0|1: bit-sliced launches deal each XCD a contiguous run of stripes (unset: rule, plan_bs)
+    kKnobBsVrow,      // MEC_BS_VROW=0|1: gathered ones fetch the pointer row in one vector load (unset: rule, 1) or per entry
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

@@ -384,7 +384,7 @@ KernelPlan plan_bm_gather(const GatherLaunch &L, uint32_t s0) {
     return p;
 }
 
-uint32_t bs_target_waves(bool in_place, bool vand) {
+uint32_t bs_target_waves(bool in_place, bool vand, bool gather) {
     // A strided bit-sliced wave streams 2 KiB of every one of its 13-28
     // chunks (32-56 KiB), 4 sources ahead; uncapped, the VGPR budget puts 12
     // such waves on a CU and the memory side queues them into lower
@@ -397,9 +397,15 @@ uint32_t bs_target_waves(bool in_place, bool vand) {
     // Cauchy(12,6) 80.6-80.7, 69 at 5; Cauchy(20,8)@4 KiB 69.2-69.9 and
     // (4,12) 75.2-76.2 would take 5 but the cliff of (12,6) rules it out),
     // in-place decodes at 8 (RS(10,6) 78.7 against 74.5 uncapped and 58 at
-    // 4-5; RS(16,8) 77.9-78.2 against 77.1).  Gathered launches stay
-    // uncapped: a cap costs them 10-37 points (their blocks first wait on
-    // the pointer row).  MEC_WPC overrides.
+    // 4-5; RS(16,8) 77.9-78.2 against 77.1).  Gathered launches at 6 once
+    // their pointer row is one vector load and each XCD takes a run of
+    // stripes (bitslice.hpp vrow / xcd): RS(16,8) batch 79.1-81.7, ISA-L
+    // RS(12,8) 80.7-80.8, RS(10,6)@256 KiB 76.1-79.4, the 8-erasure batch
+    // decode 78.7-78.8, at 5 waves 1.5-5 points lower
+    // (profiles/r05/vrow_cap_ab.jsonl); with a scalar load per entry the
+    // compiler waited on each, and any cap cost them 10-37 points.  MEC_WPC
+    // overrides.
+    if (gather) return 6;
     if (in_place) return 8;
     return vand ? 5 : 6;
 }
@@ -434,7 +440,18 @@ KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
         const uint8_t *dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
         p.win = launch_windows(src, int64_t(p.ns) * L.src_stripe_stride, dst, int64_t(p.ns) * L.dst_stripe_stride);
     }
-    p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0, L.stab ? 0u : bs_target_waves(p.win > 1, L.vand));
+    p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0, bs_target_waves(p.win > 1, L.vand, L.stab != nullptr));
+    // XCD runs: blocks are dealt round-robin over the 8 XCDs, so a stripe's
+    // blocks land on all eight and each XCD's L2 fetches its pointer row.
+    // Gathered launches of <= kBsXcdTiles blocks per stripe give each XCD a
+    // contiguous run instead (RS(16,8)@64 KiB batch +1.3-3.6 points, the
+    // 8-erasure batch decode +2.5-3.2, ISA-L RS(12,8) -1.4-+2.0); with more
+    // tiles per stripe the row is already shared (RS(10,6)@256 KiB -1.2 to
+    // -4.5), and strided launches have no row (ISA-L RS(12,8) encode -2;
+    // profiles/r05/vrow_cap_ab.jsonl, vrow_default_ab.jsonl).  MEC_BS_XCD
+    // forces it either way (never on windowed in-place launches).
+    const int64_t xk = knob(kKnobBsXcd);
+    p.xcd = p.win > 1 ? 0u : xk != kKnobUnset ? uint32_t(xk != 0) : uint32_t(L.stab && p.geo.tiles <= kBsXcdTiles);
     common_ok(p, uint64_t(p.geo.tiles) * p.tpb * 2048);
     return p;
 }

@@ -28,6 +28,9 @@ constexpr uint32_t kLdsPerCu = 160u << 10;  // gfx950: one block may take all of
 // In-place strided launches rotate stripe s's tiles by s * kTileSkew
 // (DESIGN §5.3); 0 keeps the identity order.
 constexpr int64_t kTileSkew = 0;
+// Gathered bit-sliced launches of at most this many blocks per stripe take
+// XCD runs (plan_bs).
+constexpr uint32_t kBsXcdTiles = 32;
 
 // Matrix structure a gf8 launch is specialised for (gf8_kernel.hpp).
 constexpr int kGf8Dense = 0;
@@ -69,6 +72,7 @@ struct KernelPlan {
     uint32_t win = 1, sgroup = 0, srun = 8;
     uint32_t skew = 0;       // per-stripe tile rotation (identity map, in place; MEC_TILE_SKEW)
     uint32_t tpb = 1;        // tiles per block (bit-sliced kernels: geo.tiles = blocks per stripe)
+    uint32_t xcd = 0;        // bit-sliced: blocks b, b + 8, ... (one XCD) take one run of the launch's blocks
     Geometry geo{};
     uint32_t ns = 0;         // stripes in this launch
     uint64_t grid = 0;       // blocks
@@ -191,8 +195,8 @@ KernelPlan plan_bm_gather(const GatherLaunch &L, uint32_t s0);
 KernelPlan plan_bs(const BsLaunch &L, uint32_t s0);
 // Tiles per block of a gathered bit-sliced kernel built now: MEC_BS_TPB, or 1.
 uint32_t bs_gather_tpb();
-// Resident waves per CU of a strided bit-sliced launch (plan_bs).
-uint32_t bs_target_waves(bool in_place, bool vand);
+// Resident waves per CU of a bit-sliced launch (plan_bs).
+uint32_t bs_target_waves(bool in_place, bool vand, bool gather);
 // xor_kernel over len bytes.
 KernelPlan plan_xor(uint64_t len);
 

@@ -150,6 +150,49 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 }
 __device__ __forceinline__ uint32_t uniform32(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Pointer rows of gathered launches.  A wave fetches its stripe's row in ONE
+// vector load — lane j < ns source j's entry, lane 32 + i output i's, the
+// rest 0 — and each use reads its entry back from that lane (v_readlane,
+// lane index uniform).  An entry read as a scalar load at its use made the
+// compiler wait on each in turn before that chunk's loads could issue: ten
+// dependent round trips per block before RS(10,4)'s last source load left,
+// sixteen for the bit-sliced RS(16,8) (one-map RS(16,8) batches 71.7 ->
+// 78-80 % with the row in one load, profiles/r05/vrow_ab.jsonl).
+// so / do_: the entry numbers (Gf8Params::src_off / dst_off in gather mode).
+template <int NS, int ND>
+__device__ __forceinline__ uint64_t row_fetch(const uint64_t *srow, const int64_t (&so)[NS], uint32_t ns,
+                                              const uint64_t *drow, const int64_t (&do_)[ND], uint32_t nd) {
+    // each lane picks its entry number from the (scalar) kernel arguments
+    // by compare-and-select: no per-lane read of the argument block
+    const uint32_t l = threadIdx.x & 63u;
+    const uint64_t *e = nullptr;
+#pragma unroll
+    for (int j = 0; j < NS && j < 32; ++j)
+        if (uint32_t(j) < ns && l == uint32_t(j)) e = srow + so[j];
+#pragma unroll
+    for (int i = 0; i < ND && i < 32; ++i)
+        if (uint32_t(i) < nd && l == 32u + i && do_[i] >= 0) e = drow + do_[i];
+    return e ? *e : 0;
+}
+// A gathered lane past the launch's last unit must not leave before the
+// row's v_readlanes (a lane that left no longer holds its entry): a wave
+// wholly past it leaves (uniform), a partial wave's extra lanes redo the last
+// unit — the same loads, and the same bytes stored to the same place in the
+// same instruction as the unit's own lane, read-modify-write included.
+// Returns false for a wave that leaves; u = the lane's unit.
+template <int BT>
+__device__ __forceinline__ bool gather_unit(uint32_t tile, uint32_t units, uint32_t &u) {
+    const uint32_t u0 = tile * BT + (threadIdx.x & ~63u);
+    if (u0 >= units) return false;
+    u = min(u0 + (threadIdx.x & 63u), units - 1u);
+    return true;
+}
+__device__ __forceinline__ uint64_t row_entry(uint64_t row, uint32_t lane) {
+    const uint32_t lo = __builtin_amdgcn_readlane(int(uint32_t(row)), int(lane));
+    const uint32_t hi = __builtin_amdgcn_readlane(int(uint32_t(row >> 32)), int(lane));
+    return uint64_t(hi) << 32 | lo;
+}
+
 // ---------------------------------------------------------------------------
 // partial (tail) units: < 16 bytes at the end of a region
 // ---------------------------------------------------------------------------

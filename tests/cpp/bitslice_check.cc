@@ -77,14 +77,15 @@ int main(int argc, char **argv) {
             const char *name;
             bool gather, loop;
             int prefetch;
-            bool fence;
-        } forms[] = {{"strided", false, false, 4, false}, {"gather1", true, false, 4, true},
-                     {"gather4", true, true, 4, true}, {"strided_fence", false, false, 4, true}};
+            bool fence, vrow;
+        } forms[] = {{"strided", false, false, 4, false, false}, {"gather1", true, false, 4, true, true},
+                     {"gather4", true, true, 4, true, true},     {"strided_fence", false, false, 4, true, false},
+                     {"gather1_srow", true, false, 4, true, false}};
         for (const auto &fm : forms) {
             const std::string path = std::string(argv[1]) + "/bs_" + fm.name + ".hip";
             FILE *out = std::fopen(path.c_str(), "w");
             if (!out) return 2;
-            const std::string src = bs_source(p, fm.gather, 0, fm.prefetch, fm.loop, fm.fence);
+            const std::string src = bs_source(p, fm.gather, 0, fm.prefetch, fm.loop, fm.fence, fm.vrow);
             std::fwrite(src.data(), 1, src.size(), out);
             std::fclose(out);
         }

@@ -271,7 +271,7 @@ def test_bitslice_kernels_compile_for_gfx950(tmp_path):
                            os.path.join(csrc, "bitslice.cpp"), os.path.join(csrc, "gf_math.cpp"), "-o", exe])
     out = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
-    for form in ("strided", "gather1", "gather4", "strided_fence"):
+    for form in ("strided", "gather1", "gather4", "strided_fence", "gather1_srow"):
         src = str(tmp_path / f"bs_{form}.hip")
         obj = str(tmp_path / f"bs_{form}.co")
         subprocess.check_call([hipcc, "--offload-arch=gfx950", "--cuda-device-only", "--no-gpu-bundle-output", "-O3", "-std=c++17", "-include", "hip/hip_runtime.h",

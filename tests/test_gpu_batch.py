@@ -379,3 +379,51 @@ def test_block_override_every_launch_kind(block, knobs):
         c.decode(t, sum(1 << i for i in range(k + m) if i not in (0, 4, 7)))
         torch.cuda.synchronize()
         assert np.array_equal(t.cpu().numpy(), base), (fam, block)
+
+
+@pytest.mark.parametrize("fam,k,m,bitslice", [("rs", 10, 4, None), ("cauchy", 6, 3, None), ("rs", 8, 6, "0"),
+                                              ("rs", 16, 8, "3"), ("isal_cauchy", 10, 6, "3")])
+@pytest.mark.parametrize("cs", [512, 2560])
+def test_one_map_batch_partial_wave(fam, k, m, bitslice, cs, knobs):
+    """One-map pointer batches whose last wave is partial (512-byte chunks:
+    32 of 64 lanes hold a unit; 2560: the bit-sliced kernel's second 2 KiB
+    tile half full).  Gathered kernels fetch the pointer row one entry per
+    lane (outputs in lanes 32 +) and read it back with v_readlane, so no
+    lane may leave before the last read (stream_common.hpp gather_unit):
+    gf8 (RS(10,4)), bitmatrix (Cauchy(6,3)), one-pass multi-group
+    (RS(8,6), MEC_BITSLICE=0) and bit-sliced (MEC_BITSLICE=3) launches,
+    encode then a delta update of one column, both against the oracle."""
+    knobs("MEC_BITSLICE", bitslice)
+    n = 5
+    rng = np.random.default_rng(cs + k)
+    slots = rng.permutation(n * (k + m))
+    slab = Slab(n * (k + m), cs, 8, True, 77 + k)
+    before = slab.snapshot()
+    c = Codec(fam, k, m, cs)
+    dptr, pptr = [], []
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        dptr += [slab.addr(row[j]) for j in range(k)]
+        pptr += [slab.addr(row[k + i]) for i in range(m)]
+    c.encode_batch(dptr, pptr, mem="device")
+    after = slab.snapshot()
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        par = O.encode(fam, k, m, [chunk_of(before, slab, row[j]).copy() for j in range(k)], cs)
+        for i in range(m):
+            assert np.array_equal(chunk_of(after, slab, row[k + i]), par[i]), (fam, cs, s, i)
+    # delta update of column 1 into every parity (read-modify-write gathers)
+    j = 1
+    deltas = torch.from_numpy(np.stack([O.fill(cs, 500 + s) for s in range(n)])).to(DEV)
+    c.encode_update_batch([j] * n, [deltas.data_ptr() + s * cs for s in range(n)], pptr)
+    upd = slab.snapshot()
+    dh = deltas.cpu().numpy()
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        dat = [np.zeros(cs, np.uint8) for _ in range(k)]
+        dat[j] = dh[s]
+        dp = O.encode(fam, k, m, dat, cs)
+        for i in range(m):
+            want = chunk_of(after, slab, row[k + i]) ^ dp[i]
+            assert np.array_equal(chunk_of(upd, slab, row[k + i]), want), (fam, cs, "update", s, i)
+    c.close()

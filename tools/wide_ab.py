@@ -56,6 +56,12 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "bsw12": {"MEC_BITSLICE": "3", "MEC_WPC": "12"},
         "bsnf": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0"}, "autonf": {"MEC_BITSLICE": "2", "MEC_BS_FENCE": "0"},
         "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"},
+        # gathered pointer rows: one vector load (default) / a scalar load per entry; XCD runs; row prefetch
+        "bsrow": {"MEC_BITSLICE": "3", "MEC_BS_VROW": "1"}, "bssrow": {"MEC_BITSLICE": "3", "MEC_BS_VROW": "0"},
+        "bsxcd": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "1"}, "bsnx": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "0"},
+        "bsx5": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "1", "MEC_WPC": "5"},
+        "bsx6": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "1", "MEC_WPC": "6"},
+        "bsx7": {"MEC_BITSLICE": "3", "MEC_WPC": "7"}, "bsx8": {"MEC_BITSLICE": "3", "MEC_WPC": "8"},
         # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
         "bstwin": {"MEC_BITSLICE": "3", "PROBE": "xor"}, "bsnftwin": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0", "PROBE": "xor"}}
 KNOBS = sorted({kn for a in ARMS.values() for kn in a if kn.startswith("MEC_")})
