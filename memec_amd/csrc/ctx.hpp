@@ -74,7 +74,8 @@ struct TableSlot {
     uint64_t *hdev = nullptr;  // device address of host (small zero-copy batches read it in place)
     uint64_t *dev = nullptr;
     size_t cap = 0;  // entries
-    hipEvent_t done = nullptr;
+    hipEvent_t done = nullptr;    // the launches that read dev have finished (on the caller's stream)
+    hipEvent_t copied = nullptr;  // dev holds this call's tables (on the context's copy stream)
     bool pending = false;
 };
 constexpr int kTableSlots = 4;
@@ -254,6 +255,7 @@ struct mec_ctx {
     // pointer batches (batch.cpp)
     std::mutex tab_mu;
     uint32_t tab_next = 0;
+    hipStream_t tab_stream = nullptr;  // table uploads (batch.cpp table_upload), created at first use
     mec::core::TableSlot tabs[mec::core::kTableSlots];
     mec::core::HostPipe pipe;
     mec::core::Coalescer coal;

@@ -402,7 +402,7 @@ uint32_t bs_target_waves(bool in_place, bool vand, bool gather) {
     // stripes (bitslice.hpp vrow / xcd): RS(16,8) batch 79.1-81.7, ISA-L
     // RS(12,8) 80.7-80.8, RS(10,6)@256 KiB 76.1-79.4, the 8-erasure batch
     // decode 78.7-78.8, at 5 waves 1.5-5 points lower
-    // (profiles/r05/vrow_cap_ab.jsonl); with a scalar load per entry the
+    // (profiles/r05/vrow/vrow_cap_ab_box14.jsonl); with a scalar load per entry the
     // compiler waited on each, and any cap cost them 10-37 points.  MEC_WPC
     // overrides.
     if (gather) return 6;
@@ -444,14 +444,17 @@ KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
     // XCD runs: blocks are dealt round-robin over the 8 XCDs, so a stripe's
     // blocks land on all eight and each XCD's L2 fetches its pointer row.
     // Gathered launches of <= kBsXcdTiles blocks per stripe give each XCD a
-    // contiguous run instead (RS(16,8)@64 KiB batch +1.3-3.6 points, the
-    // 8-erasure batch decode +2.5-3.2, ISA-L RS(12,8) -1.4-+2.0); with more
-    // tiles per stripe the row is already shared (RS(10,6)@256 KiB -1.2 to
-    // -4.5), and strided launches have no row (ISA-L RS(12,8) encode -2;
-    // profiles/r05/vrow_cap_ab.jsonl, vrow_default_ab.jsonl).  MEC_BS_XCD
-    // forces it either way (never on windowed in-place launches).
+    // contiguous run instead (three boxes, profiles/r05/vrow/: the 8-erasure
+    // RS(16,8)@64 KiB batch decode +2.1-3.2 points, RS(16,8) batch encode
+    // +1.2 on average, ISA-L RS(12,8) -0.4); with more tiles per stripe the
+    // row is already shared (RS(10,6)@256 KiB -1.2 to -4.5).  Strided
+    // launches take them only at <= kBsXcdStridedTiles blocks per stripe
+    // (4 KiB chunks: ISA-L Cauchy(20,8) 69.4-71.0 -> 78.0-78.7; at 64 KiB
+    // -2 to +1, at 256 KiB - 1 MiB -4.5 to -7).  MEC_BS_XCD forces it
+    // either way (never on windowed in-place launches).
     const int64_t xk = knob(kKnobBsXcd);
-    p.xcd = p.win > 1 ? 0u : xk != kKnobUnset ? uint32_t(xk != 0) : uint32_t(L.stab && p.geo.tiles <= kBsXcdTiles);
+    const uint32_t xt = L.stab ? kBsXcdTiles : kBsXcdStridedTiles;
+    p.xcd = p.win > 1 ? 0u : xk != kKnobUnset ? uint32_t(xk != 0) : uint32_t(p.geo.tiles <= xt);
     common_ok(p, uint64_t(p.geo.tiles) * p.tpb * 2048);
     return p;
 }

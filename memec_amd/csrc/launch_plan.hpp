@@ -28,9 +28,10 @@ constexpr uint32_t kLdsPerCu = 160u << 10;  // gfx950: one block may take all of
 // In-place strided launches rotate stripe s's tiles by s * kTileSkew
 // (DESIGN §5.3); 0 keeps the identity order.
 constexpr int64_t kTileSkew = 0;
-// Gathered bit-sliced launches of at most this many blocks per stripe take
-// XCD runs (plan_bs).
+// Bit-sliced launches of at most this many blocks per stripe take XCD runs
+// (plan_bs): gathered, strided.
 constexpr uint32_t kBsXcdTiles = 32;
+constexpr uint32_t kBsXcdStridedTiles = 2;
 
 // Matrix structure a gf8 launch is specialised for (gf8_kernel.hpp).
 constexpr int kGf8Dense = 0;

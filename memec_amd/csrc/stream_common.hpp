@@ -157,7 +157,7 @@ __device__ __forceinline__ uint32_t uniform32(uint32_t v) { return __builtin_amd
 // compiler wait on each in turn before that chunk's loads could issue: ten
 // dependent round trips per block before RS(10,4)'s last source load left,
 // sixteen for the bit-sliced RS(16,8) (one-map RS(16,8) batches 71.7 ->
-// 78-80 % with the row in one load, profiles/r05/vrow_ab.jsonl).
+// 78-80 % with the row in one load, profiles/r05/vrow/vrow_ab_box13.jsonl).
 // so / do_: the entry numbers (Gf8Params::src_off / dst_off in gather mode).
 template <int NS, int ND>
 __device__ __forceinline__ uint64_t row_fetch(const uint64_t *srow, const int64_t (&so)[NS], uint32_t ns,

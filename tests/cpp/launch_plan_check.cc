@@ -188,8 +188,9 @@ static void check_bs(int k, int rows, uint64_t chunk, uint32_t n, bool in_place,
         if (knob(kKnobWpc) == kKnobUnset && p.lds_dynamic * bs_target_waves(p.win > 1, vand, gather) > kLdsPerCu)
             bad("bit-sliced wave cap reserves more than a CU's LDS", p);
         if (p.xcd && p.win > 1) bad("XCD runs on a windowed launch", p);
-        if (knob(kKnobBsXcd) == kKnobUnset && p.xcd != uint32_t(gather && p.geo.tiles <= kBsXcdTiles))
-            bad("XCD runs outside the rule (gathered, <= kBsXcdTiles blocks per stripe)", p);
+        if (knob(kKnobBsXcd) == kKnobUnset &&
+            p.xcd != uint32_t(p.win <= 1 && p.geo.tiles <= (gather ? kBsXcdTiles : kBsXcdStridedTiles)))
+            bad("XCD runs outside the rule (<= kBsXcdTiles / kBsXcdStridedTiles blocks per stripe)", p);
         if (p.tpb < 1 || uint64_t(p.geo.tiles) * p.tpb * 2048 < chunk) bad("tiles do not cover the chunk", p);
         if (uint64_t(p.geo.tiles - 1) * p.tpb * 2048 >= chunk) bad("a block with no tile", p);
         covered += p.ns;
