@@ -384,7 +384,7 @@ KernelPlan plan_bm_gather(const GatherLaunch &L, uint32_t s0) {
     return p;
 }
 
-uint32_t bs_target_waves(bool in_place, bool vand, bool gather) {
+uint32_t bs_target_waves(bool in_place, bool vand, bool gather, int rows, uint32_t tiles) {
     // A strided bit-sliced wave streams 2 KiB of every one of its 13-28
     // chunks (32-56 KiB), 4 sources ahead; uncapped, the VGPR budget puts 12
     // such waves on a CU and the memory side queues them into lower
@@ -404,9 +404,13 @@ uint32_t bs_target_waves(bool in_place, bool vand, bool gather) {
     // decode 78.7-78.8, at 5 waves 1.5-5 points lower
     // (profiles/r05/vrow/vrow_cap_ab_box14.jsonl); with a scalar load per entry the
     // compiler waited on each, and any cap cost them 10-37 points.  MEC_WPC
-    // overrides.
+    // overrides.  In-place decodes of >= 8 erasures on <= 64 KiB chunks take
+    // 6 too: RS(16,8)@64 KiB 78.2 -> 79.8-80.0, ISA-L RS(12,8) 78.5 -> 80.6,
+    // RS(16,8)@4 KiB 70.9 -> 73.2, while 6-erasure decodes lose 4-5 points at
+    // 6 (RS(10,6), ISA-L Cauchy(12,6)) and so does RS(4,12)@1 MiB's decode
+    // of 12 (profiles/r05/vrow/ipcap_ab_box20.jsonl, vrow_cap_ab_box14.jsonl).
     if (gather) return 6;
-    if (in_place) return 8;
+    if (in_place) return rows >= 8 && tiles <= kBsXcdTiles ? 6 : 8;
     return vand ? 5 : 6;
 }
 
@@ -440,7 +444,7 @@ KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
         const uint8_t *dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
         p.win = launch_windows(src, int64_t(p.ns) * L.src_stripe_stride, dst, int64_t(p.ns) * L.dst_stripe_stride);
     }
-    p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0, bs_target_waves(p.win > 1, L.vand, L.stab != nullptr));
+    p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0, bs_target_waves(p.win > 1, L.vand, L.stab != nullptr, L.rows, p.geo.tiles));
     // XCD runs: blocks are dealt round-robin over the 8 XCDs, so a stripe's
     // blocks land on all eight and each XCD's L2 fetches its pointer row.
     // Gathered launches of <= kBsXcdTiles blocks per stripe give each XCD a

@@ -35,7 +35,9 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("isal_cauchy", 4, 12, 1 << 20, 512, "encode"), ("rs", 10, 6, 262144, 4096, "batch"),
           ("rs", 16, 8, 65536, 16384, "batchdec"), ("rs", 16, 8, 4096, 131072, "encode"),
           ("isal_rs", 12, 8, 4096, 131072, "encode"), ("rs", 16, 8, 4096, 131072, "batch"),
-          ("rs", 8, 6, 8192, 131072, "encode"), ("rs", 16, 8, 4096, 131072, "decode")]
+          ("rs", 8, 6, 8192, 131072, "encode"), ("rs", 16, 8, 4096, 131072, "decode"),
+          ("isal_rs", 12, 8, 65536, 16384, "decode"), ("rs", 8, 5, 16384, 32768, "decode"),
+          ("isal_cauchy", 12, 6, 65536, 16384, "decode"), ("rs", 10, 6, 65536, 16384, "decode")]
 
 
 ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
