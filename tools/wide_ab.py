@@ -37,7 +37,9 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("isal_rs", 12, 8, 4096, 131072, "encode"), ("rs", 16, 8, 4096, 131072, "batch"),
           ("rs", 8, 6, 8192, 131072, "encode"), ("rs", 16, 8, 4096, 131072, "decode"),
           ("isal_rs", 12, 8, 65536, 16384, "decode"), ("rs", 8, 5, 16384, 32768, "decode"),
-          ("isal_cauchy", 12, 6, 65536, 16384, "decode"), ("rs", 10, 6, 65536, 16384, "decode")]
+          ("isal_cauchy", 12, 6, 65536, 16384, "decode"), ("rs", 10, 6, 65536, 16384, "decode"),
+          ("rs", 8, 2, 4096, 65536, "encode"), ("rs", 8, 2, 4096, 65536, "batch"),
+          ("rs", 8, 2, 4096, 262144, "encode"), ("rs", 8, 2, 4096, 262144, "batch")]
 
 
 ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
