@@ -427,3 +427,49 @@ def test_one_map_batch_partial_wave(fam, k, m, bitslice, cs, knobs):
             want = chunk_of(after, slab, row[k + i]) ^ dp[i]
             assert np.array_equal(chunk_of(upd, slab, row[k + i]), want), (fam, cs, "update", s, i)
     c.close()
+
+
+def test_device_batches_from_threads_share_table_slots():
+    """One-map device batches large enough for the HBM table copy (> 256
+    stripes: the rows go through the context's copy stream, batch.cpp
+    table_upload) from 4 threads on one context, each on its own stream and
+    alternating between two buffer sets, so a table slot reused before its
+    launches finished would code another call's chunks.  Every call's parity
+    must equal the strided launch over the same data."""
+    k, m, cs, n, calls = 6, 3, 4096, 600, 12
+    c = Codec("rs", k, m, cs)
+    errors = []
+
+    def worker(t):
+        try:
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                sets = []
+                for b in range(2):
+                    d = torch.empty(n, k, cs, dtype=torch.uint8, device=DEV)
+                    fill_random(d, 4000 + 10 * t + b)
+                    sets.append((d, torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)))
+                ref = []
+                for d, _ in sets:
+                    r = torch.empty(n, m, cs, dtype=torch.uint8, device=DEV)
+                    c.encode(d, r, stream=st.cuda_stream)
+                    ref.append(r)
+                for i in range(calls):
+                    d, p = sets[i % 2]
+                    p.zero_()
+                    dp = [d.data_ptr() + (s * k + j) * cs for s in range(n) for j in range(k)]
+                    pp = [p.data_ptr() + (s * m + j) * cs for s in range(n) for j in range(m)]
+                    c.encode_batch(dp, pp, mem="device", stream=st.cuda_stream)
+                    st.synchronize()
+                    if not torch.equal(p, ref[i % 2]):
+                        errors.append((t, i))
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    c.close()
+    assert not errors, errors
