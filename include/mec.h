@@ -159,7 +159,10 @@ int mec_create(int family, uint32_t k, uint32_t m, uint32_t chunk_size, int devi
  * are leaked rather than freed under it, a message goes to stderr, and
  * mec_destroy returns while that kernel may still read the job's source
  * chunks and write its outputs: the caller must keep registered chunks of
- * a call that failed with MEC_EHIP alive. */
+ * a call that failed with MEC_EHIP alive.  Run-time compiles the context
+ * queued (wide codes) are cancelled; one already running is waited for, and
+ * each compiled kernel's module is unloaded after its last launch on each
+ * stream it ran on (no device-wide synchronize). */
 void mec_destroy(mec_ctx *ctx);
 /* Thread-local description of the last failure on this thread. */
 const char *mec_last_error(void);
@@ -256,7 +259,13 @@ int mec_encode_host_batch(mec_ctx *ctx, const uint8_t *data, uint8_t *parity,
  * directly on the host chunks over PCIe: no staging copy, one launch per
  * call.  A server registers its ChunkPool slab once (chunk_pool.cc:22-47,
  * the 8-byte chunk headers included); chunks outside registered ranges are
- * copied into pinned, GPU-mapped staging and coded there.  mec_host_unregister takes the same ptr. */
+ * copied into pinned, GPU-mapped staging and coded there.  Registered ranges
+ * are disjoint: a range overlapping a registered one (the same ptr included)
+ * is refused with MEC_EINVAL, so memory freed without mec_host_unregister
+ * cannot leave a stale mapping behind a later range.  mec_host_unregister
+ * takes the same ptr (MEC_EINVAL if no registered range begins there).
+ * Registration is meant for long-lived ranges: each call copies the range
+ * list and waits for concurrent lookups to leave the one it replaces. */
 int mec_host_register(void *ptr, size_t len);
 int mec_host_unregister(void *ptr);
 

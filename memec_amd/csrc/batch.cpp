@@ -505,7 +505,9 @@ int pipe_ready(mec_ctx *c, size_t bytes) {
     HostPipe &P = c->pipe;
     for (int b = 0; b < 2; ++b) {
         if (!P.stream[b]) HIP_TRY(hipStreamCreateWithFlags(&P.stream[b], hipStreamNonBlocking));
-        if (!P.done[b]) HIP_TRY(hipEventCreateWithFlags(&P.done[b], hipEventDisableTiming));
+        // system-scope release: the outputs the kernel wrote to the mapped
+        // staging are read by the host right after the wait (lane_sync)
+        if (!P.done[b]) HIP_TRY(hipEventCreateWithFlags(&P.done[b], hipEventDisableTiming | hipEventReleaseToSystem));
     }
     if (P.bytes >= bytes) return MEC_OK;
     for (int b = 0; b < 2; ++b) {
@@ -564,7 +566,7 @@ int run_zerocopy(mec_ctx *c, std::vector<Group> &gs) {
         rc = run_gather(c, M, rows[q].data(), row, rows[q].data(), row, nullptr, g.n, h.l->stream, g.n <= 256, false);
     }
     // no launch may outlive the call (the caller owns the chunks)
-    hipError_t e = lane_sync(h.l->stream);
+    hipError_t e = lane_sync(h.l);
     if (rc == MEC_OK && e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
     if (rc == MEC_OK) count_zc(c);
     return rc;
@@ -1011,11 +1013,12 @@ int mec_get_stats(const mec_ctx *cc, mec_stats *out) {
         out->mg_cache_uncached = c->mg.uncached;
     }
     {
-        std::lock_guard<std::mutex> jk(c->jit.mu);
-        out->jit_kernels = c->jit.ready;
-        out->jit_failed = c->jit.failed;
-        out->jit_pending = c->jit.pending;
-        out->jit_compile_ms = uint64_t(c->jit.compile_ms + 0.5);
+        JitShared &js = *c->jit.sh;
+        std::lock_guard<std::mutex> jk(js.mu);
+        out->jit_kernels = js.ready;
+        out->jit_failed = js.failed;
+        out->jit_pending = js.pending;
+        out->jit_compile_ms = uint64_t(js.compile_ms + 0.5);
         out->jit_launches = c->jit.launches.load();
     }
     for (mec_ctx *sc : c->shards) {  // a multi context reports its shards' sums

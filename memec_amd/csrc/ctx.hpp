@@ -60,8 +60,9 @@ struct DeviceGuard {
 // them there over PCIe (no HBM round trip, one launch per call).
 struct Lane {
     hipStream_t stream = nullptr;
-    uint8_t *host = nullptr;  // (k + m) chunk slots, pinned + mapped
-    uint8_t *hdev = nullptr;  // their device address
+    hipEvent_t done = nullptr;  // system-scope release: host memory written by the lane's launches is visible
+    uint8_t *host = nullptr;    // (k + m) chunk slots, pinned + mapped
+    uint8_t *hdev = nullptr;    // their device address
     size_t bytes = 0;
 };
 
@@ -183,15 +184,32 @@ struct JitKernel {
     double compile_ms = 0;
     std::string err;
     uint32_t tpb = 1;  // gathered: tiles per block it was built for (> 1: looped)
+    // the last launch on each stream this kernel ran on (device-scope
+    // events): jit_release waits for these, and nothing else, before it
+    // unloads the module
+    std::mutex ev_mu;
+    std::vector<std::pair<hipStream_t, hipEvent_t>> ev;
 };
-struct JitCache {
+// Shared with the compile jobs a context queued: a job may still sit in the
+// process-wide queue when its context is destroyed, so it holds this (and
+// its JitKernel) by shared_ptr; a cancelled context's queued jobs skip the
+// compile, and jit_release waits only for a compile already running.
+struct JitShared {
     std::mutex mu;
     std::condition_variable cv;
-    std::unordered_map<std::string, std::shared_ptr<JitKernel>> map;
-    size_t cap = 512;
-    uint32_t pending = 0;
+    bool cancelled = false;
+    uint32_t pending = 0;  // queued or running
+    uint32_t running = 0;
     uint64_t ready = 0, failed = 0;
     double compile_ms = 0;
+};
+struct JitCache {
+    std::mutex mu;  // the map
+    std::unordered_map<std::string, std::shared_ptr<JitKernel>> map;
+    size_t cap = 512;        // MEC_JIT_MAX_KERNELS: matrices per context
+    uint32_t max_queued = 16;  // MEC_JIT_MAX_QUEUED: compiles waiting per context
+    std::string arch = "gfx950";  // the device's gcnArchName (hiprtc --offload-arch)
+    std::shared_ptr<JitShared> sh = std::make_shared<JitShared>();
     std::atomic<uint64_t> launches{0};
 };
 
@@ -392,11 +410,15 @@ bool is_multi(const mec_ctx *c);
 mec_ctx *shard_pick(mec_ctx *c);
 int shard_run(mec_ctx *c, uint32_t n, const std::function<int(mec_ctx *, uint32_t, uint32_t)> &fn);
 
-// Wait for a lane's single-call work.  Default: hipStreamSynchronize.
-// MEC_SYNC_SPIN=1 polls hipStreamQuery for up to 200 us first: +8 % calls/s
-// for one staged caller, but -14 % at 16 workers x RS(8,2)@4K (the pollers
+// Wait for a lane's single-call work, its host-memory outputs visible to
+// the host: an event recorded with an explicit system-scope release
+// (hipEventReleaseToSystem) after the launch, then waited for — the call's
+// own completion point does not depend on how the runtime scopes a
+// kernel's end-of-dispatch release (the r05 zero-copy audit).
+// MEC_SYNC_SPIN=1 polls the event for up to 200 us first: +8 % calls/s for
+// one staged caller, but -14 % at 16 workers x RS(8,2)@4K (the pollers
 // compete for the cores the callers need) -- profiles/r01/host/sync_ab.log.
-hipError_t lane_sync(hipStream_t s);
+hipError_t lane_sync(Lane *l);
 
 // queue.hip.  queue_try: run one zero-copy call (addrs = ns sources then nd
 // outputs, device addresses) through the resident kernel; false = not

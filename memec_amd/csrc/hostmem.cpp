@@ -19,70 +19,87 @@
 // valid on every GPU, so a multi-device context shares this registry.
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <mutex>
+#include <thread>
 
 #include "ctx.hpp"
+#include "registry.hpp"
 
 namespace mec {
 namespace core {
 namespace {
 
-struct Range {
-    uintptr_t begin, end, dev;
-};
+using reg::Range;
 
-// The registry as an immutable snapshot (ranges sorted by begin), replaced
-// as a whole by mec_host_register / mec_host_unregister under reg_mu and
-// read without a lock: every zero-copy host call looks up each of its
-// chunks here, and 16 server workers taking a reader lock per chunk
-// bounced one cache line ~10^7 times a second.  A replaced snapshot is
-// retired, not freed, since a concurrent reader may still hold it; the
-// retired ones are as many as the registration calls (servers register
-// their chunk slabs once).
+// The registry as an immutable snapshot (ranges sorted by begin, disjoint),
+// replaced as a whole by mec_host_register / mec_host_unregister under
+// reg_mu and read without a lock: every zero-copy host call looks up each of
+// its chunks here, and 16 server workers taking a reader lock per chunk
+// bounced one cache line ~10^7 times a second.  Readers announce themselves
+// on one of kStripes counters (each on its own cache line; a thread keeps
+// its stripe, so with fewer threads than stripes nobody shares one) before
+// loading the snapshot pointer, and a writer that has published a new
+// snapshot frees the old one once it has seen every stripe at zero: a reader
+// that could still hold the old pointer incremented its stripe before the
+// writer's exchange (both sequentially consistent), so its count is not zero
+// until it is done (replaced snapshots were never freed).
 struct Snapshot {
     std::vector<Range> r;
 };
+constexpr size_t kStripes = 64;
+struct alignas(64) ReaderStripe {
+    std::atomic<uint64_t> n{0};
+};
+ReaderStripe g_readers[kStripes];
 std::mutex reg_mu;
 std::atomic<const Snapshot *> reg_snap{nullptr};
-std::vector<const Snapshot *> &retired() {
-    static std::vector<const Snapshot *> *v = new std::vector<const Snapshot *>;
-    return *v;
-}
 
-// Caller holds reg_mu: publish `r` as the new snapshot.
+struct ReadGuard {
+    ReaderStripe &s;
+    ReadGuard() : s(g_readers[stripe()]) { s.n.fetch_add(1, std::memory_order_seq_cst); }
+    ~ReadGuard() { s.n.fetch_sub(1, std::memory_order_release); }
+    static size_t stripe() {
+        static thread_local const size_t i = std::hash<std::thread::id>()(std::this_thread::get_id()) % kStripes;
+        return i;
+    }
+    const Snapshot *snap() const { return reg_snap.load(std::memory_order_seq_cst); }
+};
+
+// Caller holds reg_mu: publish `r` as the new snapshot and free the old one
+// once no reader can hold it.
 void publish(std::vector<Range> r) {
-    std::sort(r.begin(), r.end(), [](const Range &a, const Range &b) { return a.begin < b.begin; });
     const Snapshot *n = r.empty() ? nullptr : new Snapshot{std::move(r)};
-    const Snapshot *old = reg_snap.exchange(n, std::memory_order_acq_rel);
-    if (old) retired().push_back(old);
+    const Snapshot *old = reg_snap.exchange(n, std::memory_order_seq_cst);
+    if (!old) return;
+    for (ReaderStripe &s : g_readers)
+        while (s.n.load(std::memory_order_seq_cst) != 0) std::this_thread::yield();
+    delete old;
 }
 
-bool lookup(const Snapshot *s, uintptr_t a, size_t len, uint64_t &dev) {
-    const std::vector<Range> &v = s->r;
-    auto it = std::upper_bound(v.begin(), v.end(), a, [](uintptr_t x, const Range &g) { return x < g.begin; });
-    if (it == v.begin()) return false;
-    --it;
-    if (a < it->begin || a + len > it->end) return false;
-    dev = uint64_t(it->dev + (a - it->begin));
-    return true;
+const std::vector<Range> &ranges(const Snapshot *s) {
+    static const std::vector<Range> none;
+    return s ? s->r : none;
 }
 
 }  // namespace
 
 bool zc_device_address(const void *p, size_t len, uint64_t &dev) {
-    const Snapshot *s = reg_snap.load(std::memory_order_acquire);
-    return s && lookup(s, reinterpret_cast<uintptr_t>(p), len, dev);
+    ReadGuard g;
+    const Snapshot *s = g.snap();
+    return s && reg::lookup(s->r, reinterpret_cast<uintptr_t>(p), len, dev);
 }
 
 bool zc_any_registered() { return reg_snap.load(std::memory_order_acquire) != nullptr; }
 
 bool zc_translate(uint64_t *ptrs, size_t n, size_t len) {
-    const Snapshot *s = reg_snap.load(std::memory_order_acquire);
+    ReadGuard g;
+    const Snapshot *s = g.snap();
     if (!s) return false;
     for (size_t i = 0; i < n; ++i) {
         if (!ptrs[i]) continue;  // NULL = zero source / unwanted output
         uint64_t d;
-        if (!lookup(s, uintptr_t(ptrs[i]), len, d)) return false;
+        if (!reg::lookup(s->r, uintptr_t(ptrs[i]), len, d)) return false;
         ptrs[i] = d;
     }
     return true;
@@ -97,6 +114,20 @@ extern "C" {
 
 int mec_host_register(void *ptr, size_t len) {
     if (!ptr || !len) return fail(MEC_EINVAL, "null or empty range");
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    // held across hipHostRegister so two threads cannot both pass the
+    // overlap check with ranges that overlap each other
+    std::lock_guard<std::mutex> lk(reg_mu);
+    const std::vector<Range> &cur = ranges(reg_snap.load(std::memory_order_acquire));
+    Range hit{};
+    switch (mec::reg::can_insert(cur, a, len, &hit)) {
+        case mec::reg::Insert::kOk: break;
+        case mec::reg::Insert::kOverlap:
+            return fail(MEC_EINVAL, "[%p, +%zu) overlaps the registered range [%p, %p)%s", ptr, len,
+                        reinterpret_cast<void *>(hit.begin), reinterpret_cast<void *>(hit.end),
+                        hit.begin == a ? " (already registered)" : "; unregister it first");
+        default: return fail(MEC_EINVAL, "range [%p, +%zu) wraps the address space", ptr, len);
+    }
     HIP_TRY(hipHostRegister(ptr, len, hipHostRegisterMapped | hipHostRegisterPortable));
     void *dev = nullptr;
     hipError_t e = hipHostGetDevicePointer(&dev, ptr, 0);
@@ -104,27 +135,17 @@ int mec_host_register(void *ptr, size_t len) {
         (void)hipHostUnregister(ptr);
         return hip_fail(e, "hipHostGetDevicePointer");
     }
-    std::lock_guard<std::mutex> lk(reg_mu);
-    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
-    const Snapshot *cur = reg_snap.load(std::memory_order_acquire);
-    std::vector<Range> r;
-    if (cur)
-        for (const Range &g : cur->r)
-            if (g.begin != a) r.push_back(g);
-    r.push_back(Range{a, a + len, reinterpret_cast<uintptr_t>(dev)});
-    publish(std::move(r));
+    publish(mec::reg::with(cur, a, len, reinterpret_cast<uintptr_t>(dev)));
     return MEC_OK;
 }
 
 int mec_host_unregister(void *ptr) {
     {
         std::lock_guard<std::mutex> lk(reg_mu);
-        const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
-        const Snapshot *cur = reg_snap.load(std::memory_order_acquire);
-        std::vector<Range> r;
-        if (cur)
-            for (const Range &g : cur->r)
-                if (g.begin != a) r.push_back(g);
+        bool found = false;
+        std::vector<Range> r = mec::reg::without(ranges(reg_snap.load(std::memory_order_acquire)),
+                                                 reinterpret_cast<uintptr_t>(ptr), found);
+        if (!found) return fail(MEC_EINVAL, "%p does not begin a registered range", ptr);
         publish(std::move(r));
     }
     HIP_TRY(hipHostUnregister(ptr));

@@ -9,8 +9,13 @@
 // calls keep running on gf8_mg_kernel; once the module is loaded every later
 // call with that matrix launches it.  MEC_BITSLICE=2 compiles on the calling
 // thread at first use (benchmarks, tests), 0 never uses it.  At most
-// MEC_JIT_MAX_KERNELS (default 512) matrices per context are compiled;
-// beyond that the one-pass kernel serves them.
+// MEC_JIT_MAX_KERNELS (default 512) matrices per context are compiled, and
+// at most MEC_JIT_MAX_QUEUED (16) wait in the compile queue at once (a decode
+// workload walking many erasure patterns queues no more than that; a
+// pattern past it is queued on a later call); beyond either the one-pass
+// kernel serves the call.  mec_destroy cancels the context's queued
+// compiles, waits only for one already running and for the last launch of
+// each of its kernels on each stream, then unloads the modules.
 #include <hip/hiprtc.h>
 
 #include <chrono>
@@ -63,8 +68,8 @@ Worker &worker() {
     return *w;
 }
 
-// hiprtc source -> gfx950 code object -> module on `device`.
-void compile(JitKernel &k, const std::string &src, int device) {
+// hiprtc source -> code object for the device's arch -> module on `device`.
+void compile(JitKernel &k, const std::string &src, int device, const std::string &arch) {
     const auto t0 = std::chrono::steady_clock::now();
     hiprtcProgram prog = nullptr;
     std::string err;
@@ -72,7 +77,8 @@ void compile(JitKernel &k, const std::string &src, int device) {
     if (hiprtcCreateProgram(&prog, src.c_str(), "mec_bs.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
         err = "hiprtcCreateProgram";
     } else {
-        const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+        const std::string a = "--offload-arch=" + arch;
+        const char *opts[] = {a.c_str(), "-O3", "-std=c++17"};
         const hiprtcResult r = hiprtcCompileProgram(prog, 3, opts);
         if (r != HIPRTC_SUCCESS) {
             size_t n = 0;
@@ -174,6 +180,7 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
     key += char(vrow ? 1 : 0);
     JitCache &J = c->jit;
     const bool sync = detail::knob(detail::kKnobBitslice) >= 2;
+    const std::shared_ptr<JitShared> sh = J.sh;
     std::shared_ptr<JitKernel> k;
     bool fresh = false;
     {
@@ -183,38 +190,53 @@ JitKernel *jit_kernel(mec_ctx *c, const Mat &coef, size_t nd, size_t ns, bool ac
             k = it->second;
         } else {
             if (J.map.size() >= J.cap) return nullptr;
+            {
+                std::lock_guard<std::mutex> q(sh->mu);
+                // async: bound the compiles this context has waiting (the
+                // pattern is tried again on a later call)
+                if (!sync && sh->pending >= J.max_queued) return nullptr;
+                ++sh->pending;
+            }
             k = std::make_shared<JitKernel>();
             k->tpb = tpb;
             J.map.emplace(key, k);
             fresh = true;
-            ++J.pending;
         }
     }
     if (fresh) {
         auto src = std::make_shared<std::string>(bs_source(twin ? bs_build_twin(int(nd), int(ns), accumulate) : bs_build(coef.data(), int(nd), int(ns), accumulate),
                       gather, waves, prefetch, loop, fence, vrow));
         const int device = c->device;
-        auto done = [&J, k] {
-            std::lock_guard<std::mutex> g(J.mu);
-            --J.pending;
-            J.compile_ms += k->compile_ms;
-            if (k->state.load() > 0) ++J.ready;
-            else ++J.failed;
-            J.cv.notify_all();
+        const std::string arch = J.arch;
+        // a job runs unless its context was released meanwhile; it holds
+        // the shared state and the kernel, never the context
+        auto job = [k, src, device, arch, sh] {
+            {
+                std::lock_guard<std::mutex> g(sh->mu);
+                if (sh->cancelled) {
+                    --sh->pending;
+                    k->err = "context released before the compile ran";
+                    k->state.store(-1, std::memory_order_release);
+                    sh->cv.notify_all();
+                    return;
+                }
+                ++sh->running;
+            }
+            compile(*k, *src, device, arch);
+            std::lock_guard<std::mutex> g(sh->mu);
+            --sh->running;
+            --sh->pending;
+            sh->compile_ms += k->compile_ms;
+            if (k->state.load() > 0) ++sh->ready;
+            else ++sh->failed;
+            sh->cv.notify_all();
         };
-        if (sync) {
-            compile(*k, *src, device);
-            done();
-        } else {
-            worker().post([k, src, device, done] {
-                compile(*k, *src, device);
-                done();
-            });
-        }
+        if (sync) job();
+        else worker().post(job);
     }
     if (sync && k->state.load(std::memory_order_acquire) == 0) {  // another thread compiling it: wait
-        std::unique_lock<std::mutex> g(J.mu);
-        J.cv.wait(g, [&] { return k->state.load(std::memory_order_acquire) != 0; });
+        std::unique_lock<std::mutex> g(sh->mu);
+        sh->cv.wait(g, [&] { return k->state.load(std::memory_order_acquire) != 0; });
     }
     return k->state.load(std::memory_order_acquire) > 0 ? k.get() : nullptr;
 }
@@ -251,25 +273,49 @@ int jit_launch(mec_ctx *c, JitKernel *k, const BsLaunch &L0, hipStream_t stream)
         HIP_TRY(hipModuleLaunchKernel(k->fn, uint32_t(pl.grid), 1, 1, pl.bt, 1, 1, pl.lds_dynamic, stream, nullptr, cfg));
         s0 += pl.ns;
     }
+    {  // the module's last launch on this stream (jit_release waits for it)
+        std::lock_guard<std::mutex> g(k->ev_mu);
+        hipEvent_t ev = nullptr;
+        for (auto &pr : k->ev)
+            if (pr.first == stream) ev = pr.second;
+        if (!ev) {
+            HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice));
+            k->ev.emplace_back(stream, ev);
+        }
+        HIP_TRY(hipEventRecord(ev, stream));
+    }
     c->jit.launches.fetch_add(1, std::memory_order_relaxed);
     return MEC_OK;
 }
 
-void jit_init(mec_ctx *c) { c->jit.cap = size_t(env_u64("MEC_JIT_MAX_KERNELS", 512)); }
+void jit_init(mec_ctx *c) {
+    c->jit.cap = size_t(env_u64("MEC_JIT_MAX_KERNELS", 512));
+    c->jit.max_queued = uint32_t(std::max<uint64_t>(1, env_u64("MEC_JIT_MAX_QUEUED", 16)));
+}
 
+// no device-wide synchronize (it waited on every stream of the
+// device, other contexts' resident queue grids and a hung one included):
+// queued compiles are cancelled, a running one is waited for, and each
+// module is unloaded after the last launch it made on each stream.
 void jit_release(mec_ctx *c) {
     JitCache &J = c->jit;
     {
-        std::unique_lock<std::mutex> g(J.mu);
-        J.cv.wait(g, [&] { return J.pending == 0; });
+        std::unique_lock<std::mutex> g(J.sh->mu);
+        J.sh->cancelled = true;
+        J.sh->cv.wait(g, [&] { return J.sh->running == 0; });
     }
-    bool any = false;
-    for (auto &kv : J.map) any = any || kv.second->mod;
-    if (any) {
-        DeviceGuard dg(c->device);
-        (void)hipDeviceSynchronize();  // no launch of a module may still run
-        for (auto &kv : J.map)
-            if (kv.second->mod) (void)hipModuleUnload(kv.second->mod);
+    DeviceGuard dg(c->device);
+    for (auto &kv : J.map) {
+        JitKernel &k = *kv.second;
+        std::lock_guard<std::mutex> g(k.ev_mu);
+        for (auto &pr : k.ev) {
+            (void)hipEventSynchronize(pr.second);
+            (void)hipEventDestroy(pr.second);
+        }
+        k.ev.clear();
+        if (k.mod) (void)hipModuleUnload(k.mod);
+        k.mod = nullptr;
+        k.fn = nullptr;
     }
     J.map.clear();
 }

@@ -148,9 +148,10 @@ int apply(mec_ctx *c, const Layout &lay, const Mat &coef, uint32_t n_stripes, bo
         return MEC_OK;
     }
     const bool probe = c->probe.load(std::memory_order_relaxed) == MEC_PROBE_XOR;
-    if (jit_wanted(c, nd, ns, coef, false)) {
+    if (mg_wanted(c, nd) && jit_wanted(c, nd, ns, coef, false)) {
         // more than 4 outputs: the matrix's own bit-sliced kernel once built
-        // (its arithmetic-free twin under MEC_PROBE_XOR)
+        // (its arithmetic-free twin under MEC_PROBE_XOR); MEC_WIDE=0 turns
+        // every one-pass form off, as on the pointer-batch path (run_gather)
         if (JitKernel *jk = jit_kernel(c, coef, nd, ns, accumulate, false, probe)) {
             mec::BsLaunch L{};
             L.src = lay.src;
@@ -316,11 +317,13 @@ Lane *lane_acquire(mec_ctx *c, int &rc) {
     Lane *l = new Lane;
     l->bytes = size_t(c->k + c->m) * c->cs;
     hipError_t e = hipStreamCreateWithFlags(&l->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&l->done, hipEventDisableTiming | hipEventReleaseToSystem);
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&l->host), l->bytes, hipHostMallocMapped);
     if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void **>(&l->hdev), l->host, 0);
     if (e != hipSuccess) {
         rc = hip_fail(e, "staging lane");
         if (l->host) (void)hipHostFree(l->host);
+        if (l->done) (void)hipEventDestroy(l->done);
         if (l->stream) (void)hipStreamDestroy(l->stream);
         delete l;
         return nullptr;
@@ -330,19 +333,21 @@ Lane *lane_acquire(mec_ctx *c, int &rc) {
     return l;
 }
 
-hipError_t lane_sync(hipStream_t s) {
+hipError_t lane_sync(Lane *l) {
     static const bool spin = [] {
         const char *e = std::getenv("MEC_SYNC_SPIN");
         return e && e[0] && e[0] != '0';
     }();
+    const hipError_t r = hipEventRecord(l->done, l->stream);
+    if (r != hipSuccess) return r;
     if (spin) {
         const auto t0 = std::chrono::steady_clock::now();
         while (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200)) {
-            const hipError_t e = hipStreamQuery(s);
+            const hipError_t e = hipEventQuery(l->done);
             if (e != hipErrorNotReady) return e;
         }
     }
-    return hipStreamSynchronize(s);
+    return hipEventSynchronize(l->done);
 }
 
 void lane_release(mec_ctx *c, Lane *l) {
@@ -388,7 +393,7 @@ int zc_single(mec_ctx *c, const std::vector<const uint8_t *> &srcs, const std::v
     uint8_t *b = reinterpret_cast<uint8_t *>(uintptr_t(base));
     rc = apply(c, b, 0, so, b, 0, dof, coef, 1, accumulate, h.l->stream);
     if (rc != MEC_OK) return rc;
-    HIP_TRY(lane_sync(h.l->stream));
+    HIP_TRY(lane_sync(h.l));
     count_zc(c);
     return MEC_OK;
 }
@@ -416,7 +421,7 @@ int lane_run(mec_ctx *c, LaneHold &h, const std::vector<int64_t> &so, const std:
     }
     int rc = apply(c, l->hdev, 0, so, l->hdev, 0, dof, coef, 1, accumulate, l->stream);
     if (rc != MEC_OK) return rc;
-    HIP_TRY(lane_sync(l->stream));
+    HIP_TRY(lane_sync(l));
     return MEC_OK;
 }
 
@@ -490,6 +495,7 @@ int mec_create(int family, uint32_t k, uint32_t m, uint32_t chunk_size, int devi
         if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
         if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
             return fail(MEC_ENODEV, "device %d is %s; libmec is built for gfx950 only", device, prop.gcnArchName);
+        c->jit.arch = prop.gcnArchName;  // hiprtc compiles for exactly this target
     }
     *out = c.release();
     return MEC_OK;
@@ -510,6 +516,7 @@ void mec_destroy(mec_ctx *c) {
             if (!drained) break;
             (void)hipStreamSynchronize(l->stream);
             (void)hipHostFree(l->host);
+            (void)hipEventDestroy(l->done);
             (void)hipStreamDestroy(l->stream);
             delete l;
         }
@@ -785,11 +792,15 @@ int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint
         std::vector<int64_t> so(c->k), dof(rows.size());
         for (uint32_t j = 0; j < c->k; ++j) so[j] = int64_t(j) * int64_t(cs);
         for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(rows[r]) * int64_t(cs);
-        int rc = apply(c, reinterpret_cast<const uint8_t *>(uintptr_t(zd)), int64_t(dbytes), so,
-                       reinterpret_cast<uint8_t *>(uintptr_t(zp)), int64_t(pbytes), dof, encode_rows(c, rows, cols),
-                       n_stripes, false, c->bstream[0]);
+        int rc = MEC_OK;
+        LaneHold h{c, lane_acquire(c, rc)};
+        if (!h.l) return rc;
+        rc = apply(c, reinterpret_cast<const uint8_t *>(uintptr_t(zd)), int64_t(dbytes), so,
+                   reinterpret_cast<uint8_t *>(uintptr_t(zp)), int64_t(pbytes), dof, encode_rows(c, rows, cols),
+                   n_stripes, false, h.l->stream);
+        const hipError_t e = lane_sync(h.l);  // no launch may outlive the call (the caller owns the buffers)
         if (rc != MEC_OK) return rc;
-        HIP_TRY(hipStreamSynchronize(c->bstream[0]));
+        HIP_TRY(e);
         count_zc(c);
         return MEC_OK;
     }

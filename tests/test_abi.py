@@ -281,3 +281,35 @@ def test_bitslice_kernels_compile_for_gfx950(tmp_path):
         scratch = int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", notes).group(1))
         assert scratch == 0, (form, scratch)
         assert vgpr <= (168 if form == "strided" else 128), (form, vgpr)
+
+
+def test_registry_ranges_disjoint(tmp_path):
+    """tests/cpp/registry_check.cc: the zero-copy registry
+    (memec_amd/csrc/registry.hpp, hostmem.cpp) refuses a range that overlaps
+    a registered one — re-registration and a range that starts below a
+    registered one and extends across it included —
+    unregisters by begin only, and translates an address only inside one
+    range; random register / unregister / lookup sequences against a
+    brute-force model (ASan + UBSan)."""
+    import shutil
+    import subprocess
+    if not shutil.which("g++"):
+        pytest.skip("g++ not available")
+    exe = str(tmp_path / "registry_check")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                           "-I" + os.path.join(ROOT, "memec_amd", "csrc"),
+                           os.path.join(ROOT, "tests", "cpp", "registry_check.cc"), "-o", exe])
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-2000:]
+    assert out.stdout.startswith("ok "), out.stdout
+
+
+def test_unregister_unknown_range_is_refused():
+    """mec_host_unregister of a pointer that begins no registered range is
+    MEC_EINVAL before any HIP call (so it holds on a host without a GPU)."""
+    import ctypes
+    L = _lib.lib()
+    buf = ctypes.create_string_buffer(4096)
+    assert L.mec_host_unregister(ctypes.cast(buf, ctypes.c_void_p)) == _lib.MEC_EINVAL
+    assert b"does not begin a registered range" in L.mec_last_error()
+    assert L.mec_host_register(None, 16) == _lib.MEC_EINVAL

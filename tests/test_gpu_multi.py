@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import _oracle as O
+from _mismatch import same
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -57,7 +58,7 @@ def test_multi_encode_decode_update_batches(fam, registered):
         want = [O.encode(fam, k, m, data[s], cs) for s in range(n)]
         for s in range(n):
             for i in range(m):
-                assert np.array_equal(view(s, k + i), want[s][i]), (s, i)
+                same(view(s, k + i), want[s][i], (s, i))
         # decode: a different pattern per stripe, including > m in two shards
         rng = np.random.default_rng(4)
         pats, masks = [], []
@@ -78,7 +79,7 @@ def test_multi_encode_decode_update_batches(fam, registered):
             else:
                 assert res[s] == 0, (s, res[s])
             for i in range(k + m):
-                assert np.array_equal(view(s, i), orig[s][i]), (s, pats[s], i)
+                same(view(s, i), orig[s][i], (s, pats[s], i))
         # delta update, mixed columns
         js = [int(rng.integers(0, k)) for _ in range(n)]
         deltas = aligned(n * cs).reshape(n, cs)
@@ -96,7 +97,7 @@ def test_multi_encode_decode_update_batches(fam, registered):
             d2[js[s]] ^= deltas[s]
             w2 = O.encode(fam, k, m, d2, cs)
             for i in range(m):
-                assert np.array_equal(view(s, k + i), w2[i]), (s, i)
+                same(view(s, k + i), w2[i], (s, i))
         st = c.stats()
         if registered:
             assert st["zero_copy_calls"] >= 9 and st["staged_calls"] == 0  # 3 calls x 3 shards
@@ -115,19 +116,19 @@ def test_multi_dense_batch_and_single_stripe_calls():
     p = np.zeros((n, m, cs), np.uint8)
     c.encode_host_batch(d, p)
     for s in range(n):
-        assert np.array_equal(p[s], np.stack(O.encode("rs", k, m, list(d[s]), cs))), s
+        same(p[s], np.stack(O.encode("rs", k, m, list(d[s]), cs)), s)
     # single-stripe calls alternate between the shards
     for s in range(4):
         got = c.encode_host(list(d[s]))
         for i in range(m):
-            assert np.array_equal(got[i], p[s, i])
+            same(got[i], p[s, i], "")
     assert c.stats()["staged_calls"] >= 2 + 4
     # device-memory calls run on devices[0]
     dd = torch.from_numpy(d.copy()).to("cuda:0")
     pp = torch.zeros(n, m, cs, dtype=torch.uint8, device="cuda:0")
     c.encode(dd, pp)
     torch.cuda.synchronize()
-    assert np.array_equal(pp.cpu().numpy(), p)
+    same(pp.cpu().numpy(), p, "")
     c.close()
 
 

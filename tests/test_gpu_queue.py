@@ -19,6 +19,7 @@ import numpy as np
 import pytest
 
 import _oracle as O
+from _mismatch import same
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -131,7 +132,7 @@ def _encode_decode_update(fam, k, m, cs, parts=None, slots=8):
         for i in range(m):  # the SEAL pattern: encode(index) for every parity
             encode_index(c, slab, k, list(range(k)), k + i, i + 1)
         for i in range(m):
-            assert np.array_equal(slab.view(k + i), want[i]), (fam, i)
+            same(slab.view(k + i), want[i], (fam, i))
         assert c.stats()["queue_calls"] == q0 + m
         # Coding::zeros sources (NULL) in a single-column encode
         single = [None] * k
@@ -140,7 +141,7 @@ def _encode_decode_update(fam, k, m, cs, parts=None, slots=8):
         z = [np.zeros(cs, np.uint8)] * k
         z = list(z)
         z[2] = data[2].copy()
-        assert np.array_equal(slab.view(k + m), O.encode(fam, k, m, z, cs)[0])
+        same(slab.view(k + m), O.encode(fam, k, m, z, cs)[0], "")
         # decode in place, data and parity erased
         orig = [slab.view(i).copy() for i in range(k + m)]
         pat = sorted({0, k - 1, k, k + m - 1})[:m]
@@ -148,7 +149,7 @@ def _encode_decode_update(fam, k, m, cs, parts=None, slots=8):
             slab.view(e)[:] = 0
         c.decode_host([slab.view(i) for i in range(k + m)], sum(1 << i for i in range(k + m) if i not in pat))
         for i in range(k + m):
-            assert np.array_equal(slab.view(i), orig[i]), (fam, pat, i)
+            same(slab.view(i), orig[i], (fam, pat, i))
         # delta update of every parity (the spare slot holds the delta)
         delta = slab.view(k + m)
         d2 = [o.copy() for o in orig[:k]]
@@ -156,7 +157,7 @@ def _encode_decode_update(fam, k, m, cs, parts=None, slots=8):
         c.encode_update_host(1, delta, [slab.view(k + i) for i in range(m)])
         want2 = O.encode(fam, k, m, d2, cs)
         for i in range(m):
-            assert np.array_equal(slab.view(k + i), want2[i]), (fam, i)
+            same(slab.view(k + i), want2[i], (fam, i))
         st = c.stats()
         assert st["queue_calls"] == q0 + m + 3 and st["queue_launches"] >= 1
     finally:
@@ -303,7 +304,7 @@ def test_queue_idle_exit_and_relaunch():
         for rnd in range(4):
             slab.view(k)[:] = 0
             encode_index(c, slab, k, list(range(k)), k, 1)
-            assert np.array_equal(slab.view(k), want[0]), rnd
+            same(slab.view(k), want[0], rnd)
             time.sleep(0.05)  # > idle: the resident kernel exits
         st = c.stats()
         assert st["queue_calls"] == 4 and st["queue_launches"] >= 2
@@ -349,7 +350,7 @@ def test_queue_quiet_slot_beside_busy_slot():
             dt = time.perf_counter() - t0
             if dt > 0.5:
                 slow.append((rnd, dt))
-            assert np.array_equal(slab.view(b + k + 1), wants[1][1]), rnd
+            same(slab.view(b + k + 1), wants[1][1], rnd)
         stop.set()
         th.join()
         assert not errs, errs[:5]
@@ -378,7 +379,7 @@ def test_queue_timeout_withdraws_and_falls_back(fam):
             for i in range(m):
                 slab.view(k + i)[:] = 0
                 encode_index(c, slab, k, list(range(k)), k + i, i + 1)
-                assert np.array_equal(slab.view(k + i), want[i]), (rnd, i)
+                same(slab.view(k + i), want[i], (rnd, i))
         st = c.stats()
         assert st["queue_broken"] and st["queue_timeouts"] >= 1
         assert st["queue_calls"] <= 1  # at most the first call, if it beat the withdrawal
@@ -388,7 +389,7 @@ def test_queue_timeout_withdraws_and_falls_back(fam):
         got = c.encode_host(data)
         w2 = O.encode(fam, k, m, [d.copy() for d in data], cs)
         for i in range(m):
-            assert np.array_equal(got[i], w2[i])
+            same(got[i], w2[i], "")
     finally:
         os.environ.pop("MEC_QUEUE_TIMEOUT_MS", None)
         c.close()
@@ -414,7 +415,7 @@ def test_queue_timeout_multipart_all_or_nothing(fam):
         for i in range(m):
             slab.view(k + i)[:] = 0
             encode_index(c, slab, k, list(range(k)), k + i, i + 1)
-            assert np.array_equal(slab.view(k + i), want[i]), i
+            same(slab.view(k + i), want[i], i)
         # accumulate: parity ^= A[:, 2] * delta, twice -> back to `want`, and
         # once more -> the encode of data with column 2 ^= delta
         delta = slab.view(k + m)
@@ -424,7 +425,7 @@ def test_queue_timeout_multipart_all_or_nothing(fam):
         d2[2] ^= delta
         want2 = O.encode(fam, k, m, d2, cs)
         for i in range(m):
-            assert np.array_equal(slab.view(k + i), want2[i]), i
+            same(slab.view(k + i), want2[i], i)
         st = c.stats()
         assert st["queue_broken"] and st["queue_timeouts"] >= 1
     finally:
@@ -444,12 +445,12 @@ def test_queue_fallbacks():
         c.set_host_queue(4)
         want = O.encode("rs", k, m, [slab.view(j).copy() for j in range(k)], cs)
         encode_index(c, slab, k, list(range(k)), k + 1, 2)
-        assert np.array_equal(slab.view(k + 1), want[1])
+        same(slab.view(k + 1), want[1], "")
         assert c.stats()["queue_calls"] == 0
         c.set_host_queue(0)
         slab.view(k + 1)[:] = 0
         encode_index(c, slab, k, list(range(k)), k + 1, 2)
-        assert np.array_equal(slab.view(k + 1), want[1])
+        same(slab.view(k + 1), want[1], "")
     finally:
         c.close()
         slab.close()
@@ -462,7 +463,7 @@ def test_queue_fallbacks():
         got = c.encode_host(data)
         want = O.encode("rs", k, m, [d.copy() for d in data], cs)
         for i in range(m):
-            assert np.array_equal(got[i], want[i])
+            same(got[i], want[i], "")
         st = c.stats()
         assert st["queue_calls"] == 0 and st["staged_calls"] == 1
     finally:
@@ -484,14 +485,14 @@ def test_queue_staged_calls(fam, k, m, cs):
             want = O.encode(fam, k, m, [d.copy() for d in data], cs)
             got = c.encode_host(data)
             for i in range(m):
-                assert np.array_equal(got[i], want[i]), (rnd, i)
+                same(got[i], want[i], (rnd, i))
             chunks = [d.copy() for d in data] + [w.copy() for w in want]
             pat = sorted({rnd % k, k - 1, k + rnd % m})[:m]
             for e in pat:
                 chunks[e][:] = 0
             c.decode_host(chunks, sum(1 << i for i in range(k + m) if i not in pat))
             for i in range(k + m):
-                assert np.array_equal(chunks[i], data[i] if i < k else want[i - k]), (rnd, pat, i)
+                same(chunks[i], data[i] if i < k else want[i - k], (rnd, pat, i))
             delta = O.fill(cs, 7777 + rnd)
             par = [w.copy() for w in want]
             c.encode_update_host(rnd % k, delta, par)
@@ -499,7 +500,7 @@ def test_queue_staged_calls(fam, k, m, cs):
             d2[rnd % k] ^= delta
             want2 = O.encode(fam, k, m, d2, cs)
             for i in range(m):
-                assert np.array_equal(par[i], want2[i]), (rnd, i)
+                same(par[i], want2[i], (rnd, i))
         st = c.stats()
         assert st["queue_calls"] - st0["queue_calls"] == 18
         assert st["staged_calls"] - st0["staged_calls"] == 18

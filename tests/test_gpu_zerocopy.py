@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import _oracle as O
+from _mismatch import same
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -85,19 +86,20 @@ def test_zc_encode_batch(fam, cs):
             data = [zeros(cs) if j in zc else slab.view(row[j]).copy() for j in range(k)]
             want.append((row, wanted, O.encode(fam, k, m, data, cs)))
         z0 = c.stats()["zero_copy_calls"]
+        pre = slab.buf.copy()
         c.encode_batch(dptr, pptr, mem="host")
         assert c.stats()["zero_copy_calls"] == z0 + 1
         for s, (row, wanted, par) in enumerate(want):
             for i in range(m):
                 o = row[k + i] * slab.slot + slab.hdr
                 exp = par[i] if wanted[i] else before[o:o + cs]
-                assert np.array_equal(slab.view(row[k + i]), exp), (fam, s, i)
+                same(slab.view(row[k + i]), exp, (fam, s, i), before=pre[o:o + cs], addr=slab.addr(row[k + i]))
         # headers and sources untouched
         for s in range(n):
             row = slots[s * (k + m):(s + 1) * (k + m)]
             for j in range(k):
                 o = row[j] * slab.slot
-                assert np.array_equal(slab.buf[o:o + slab.slot], before[o:o + slab.slot])
+                same(slab.buf[o:o + slab.slot], before[o:o + slab.slot], ("source", s, j))
     finally:
         slab.close()
 
@@ -117,6 +119,10 @@ def test_zc_decode_batch_mixed(fam):
             pats.append(pat)
             ptrs += [slab.addr(s * (k + m) + i) for i in range(k + m)]
             masks.append(sum(1 << i for i in range(k + m) if i not in pat))
+        for s in range(n):
+            for e in pats[s]:
+                slab.view(s * (k + m) + e)[:] = 0
+        pre = [slab.view(i).copy() for i in range(n * (k + m))]
         assert c.decode_batch(ptrs, masks, mem="host") == [0] * n
         assert c.stats()["zero_copy_calls"] >= 1
         for s in range(n):
@@ -124,7 +130,8 @@ def test_zc_decode_batch_mixed(fam):
             if pats[s]:
                 assert O.decode(fam, k, m, chunks, pats[s], cs) == 0
             for i in range(k + m):
-                assert np.array_equal(slab.view(s * (k + m) + i), chunks[i]), (fam, s, pats[s], i)
+                same(slab.view(s * (k + m) + i), chunks[i], (fam, s, pats[s], i), before=pre[s * (k + m) + i],
+                     addr=slab.addr(s * (k + m) + i))
     finally:
         slab.close()
 
@@ -145,6 +152,7 @@ def test_zc_update_batch(fam):
         js = [int(rng.integers(0, k)) for _ in range(n)]
         c = Codec(fam, k, m, cs)
         pb, db = P.ctypes.data, D.ctypes.data
+        pre = P.copy()
         c.encode_update_batch(js, [db + s * cs for s in range(n)],
                               [pb + (s * m + i) * cs for s in range(n) for i in range(m)], mem="host")
         assert c.stats()["zero_copy_calls"] == 1
@@ -153,7 +161,7 @@ def test_zc_update_batch(fam):
             d2[js[s]] ^= D[s]
             want = O.encode(fam, k, m, list(d2), cs)
             for i in range(m):
-                assert np.array_equal(P[s, i], want[i]), (fam, s, i)
+                same(P[s, i], want[i], (fam, s, i), before=pre[s, i], addr=P[s, i].ctypes.data)
         assert not np.array_equal(P, p0)
     finally:
         host_unregister(P)
@@ -163,7 +171,8 @@ def test_zc_update_batch(fam):
 @pytest.mark.parametrize("fam", FAMS)
 def test_zc_single_stripe_calls(fam):
     """mec_encode_host / mec_decode_host / mec_encode_update_host on slab
-    chunks: one launch on the chunks' device addresses."""
+    chunks: one launch on the chunks' device addresses.  Every comparison
+    reports a mismatch map (tests/_mismatch.py) against the pre-call bytes."""
     k, m = 10, 4
     cs = cs_for(fam, k, m, 65536)
     slab = HostSlab(k + m + 1, cs, 9)
@@ -174,7 +183,7 @@ def test_zc_single_stripe_calls(fam):
         want = O.encode(fam, k, m, [d.copy() for d in data], cs)
         got = c.encode_host(data)  # outputs are fresh (unregistered) arrays: staged
         for i in range(m):
-            assert np.array_equal(got[i], want[i])
+            same(got[i], want[i], ("staged encode", fam, i))
         st0 = c.stats()
         # in-place parity into the slab: zero-copy
         import ctypes
@@ -182,26 +191,31 @@ def test_zc_single_stripe_calls(fam):
         vp = ctypes.c_void_p
         dp = (vp * k)(*[vp(slab.addr(j)) for j in range(k)])
         pp = (vp * m)(*[vp(slab.addr(k + i)) for i in range(m)])
+        pre = [p.copy() for p in par]
         check(lib().mec_encode_host(c._h, dp, pp))
         for i in range(m):
-            assert np.array_equal(par[i], want[i]), i
+            same(par[i], want[i], ("zc encode", fam, i), before=pre[i], addr=slab.addr(k + i))
         assert c.stats()["zero_copy_calls"] == st0["zero_copy_calls"] + 1
         # decode in place: erase a mix of data and parity
         orig = [slab.view(i).copy() for i in range(k + m)]
         pat = [0, 3, 10, 13]
         for e in pat:
             slab.view(e)[:] = 0
+        pre = [slab.view(i).copy() for i in range(k + m)]
         c.decode_host([slab.view(i) for i in range(k + m)], sum(1 << i for i in range(k + m) if i not in pat))
         for i in range(k + m):
-            assert np.array_equal(slab.view(i), orig[i]), i
+            same(slab.view(i), orig[i], ("zc decode", fam, pat, i), before=pre[i], addr=slab.addr(i))
         # delta update of two parities, the delta in the slab's spare slot
         delta = slab.view(k + m)
         d2 = [o.copy() for o in orig[:k]]
         d2[4] ^= delta
         want2 = O.encode(fam, k, m, d2, cs)
+        pre = [p.copy() for p in par]
         c.encode_update_host(4, delta, [par[0], None, par[2], None])
-        assert np.array_equal(par[0], want2[0]) and np.array_equal(par[2], want2[2])
-        assert np.array_equal(par[1], orig[k + 1]) and np.array_equal(par[3], orig[k + 3])
+        same(par[0], want2[0], ("zc update", fam, 0), before=pre[0], addr=slab.addr(k))
+        same(par[2], want2[2], ("zc update", fam, 2), before=pre[2], addr=slab.addr(k + 2))
+        same(par[1], orig[k + 1], ("zc update untouched", fam, 1), addr=slab.addr(k + 1))
+        same(par[3], orig[k + 3], ("zc update untouched", fam, 3), addr=slab.addr(k + 3))
         assert c.stats()["zero_copy_calls"] == st0["zero_copy_calls"] + 3
     finally:
         slab.close()
@@ -233,7 +247,8 @@ def test_zc_host_batch_dense(fam):
         c.encode_host_batch(d, p)
         assert c.stats()["zero_copy_calls"] == 1
         for s in range(n):
-            assert np.array_equal(p[s], np.stack(O.encode(fam, k, m, list(d[s]), cs))), s
+            same(p[s], np.stack(O.encode(fam, k, m, list(d[s]), cs)), ("zc host batch", fam, s), before=np.zeros_like(p[s]),
+                 addr=p[s].ctypes.data)
     finally:
         host_unregister(d)
         host_unregister(p)
@@ -258,7 +273,7 @@ def test_zc_partial_registration_falls_back():
                 data[1] = outside
             want = O.encode("rs", k, m, data, cs)
             for i in range(m):
-                assert np.array_equal(slab.view(s * (k + m) + k + i), want[i]), (s, i)
+                same(slab.view(s * (k + m) + k + i), want[i], ("staged fallback", s, i), addr=slab.addr(s * (k + m) + k + i))
     finally:
         slab.close()
 
@@ -287,7 +302,8 @@ def test_zc_coalesced_threads():
                 errors.append(("rc", t, r))
             for i in range(m):
                 if not np.array_equal(slab.view(base + k + i), want[i]):
-                    errors.append((t, r, i))
+                    from _mismatch import mismatch_map
+                    errors.append((t, r, i, mismatch_map(slab.view(base + k + i), want[i], addr=slab.addr(base + k + i))))
 
     try:
         th = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
@@ -301,3 +317,45 @@ def test_zc_coalesced_threads():
         assert st["zero_copy_calls"] == st["coalesced_batches"] and st["staged_calls"] == 0
     finally:
         slab.close()
+
+
+def test_zc_register_overlap_refused():
+    """a range overlapping a registered one is refused
+    (MEC_EINVAL) — the same begin, inside it, and one that starts below it
+    and extends across it — while a disjoint neighbour registers, and after
+    unregistering the first range the overlapping one registers and codes
+    zero-copy, exactly."""
+    from memec_amd import _lib
+    k, m, cs = 4, 2, 4096
+    big = aligned(64 * 4096)
+    big[:] = O.fill(big.nbytes, 17)
+    inner = big[16 * 4096:32 * 4096]
+    lo = big[8 * 4096:24 * 4096]          # starts below `inner`, extends across it
+    nb = big[40 * 4096:48 * 4096]         # disjoint neighbour
+    host_register(inner)
+    try:
+        for arr in (inner, inner[4096:8192], lo):
+            with pytest.raises(_lib.MecError) as ei:
+                host_register(arr)
+            assert ei.value.code == _lib.MEC_EINVAL
+        host_register(nb)
+        host_unregister(nb)
+    finally:
+        host_unregister(inner)
+    with pytest.raises(_lib.MecError):
+        host_unregister(inner)            # no longer registered
+    host_register(lo)
+    try:
+        c = Codec("rs", k, m, cs)
+        base = lo.ctypes.data
+        data = [lo[j * cs:(j + 1) * cs] for j in range(k)]
+        par = [lo[(k + i) * cs:(k + i + 1) * cs] for i in range(m)]
+        want = O.encode("rs", k, m, [d.copy() for d in data], cs)
+        pre = [p.copy() for p in par]
+        z0 = c.stats()["zero_copy_calls"]
+        c.encode_batch([base + j * cs for j in range(k)], [base + (k + i) * cs for i in range(m)], mem="host")
+        assert c.stats()["zero_copy_calls"] == z0 + 1
+        for i in range(m):
+            same(par[i], want[i], ("overlap re-register", i), before=pre[i], addr=base + (k + i) * cs)
+    finally:
+        host_unregister(lo)

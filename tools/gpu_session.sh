@@ -43,6 +43,7 @@ for step in "$@"; do
         bounds)  # the bounds-checked build (make -C memec_amd bounds) under the index-heavy suites
             run pytest_bounds 900 env MEMEC_LIBMEC=memec_amd/bounds/libmec.so python -u -m pytest tests/test_gpu_wide.py \
                 tests/test_gpu_batch.py tests/test_gpu_sweep.py tests/test_gpu_queue.py tests/test_gpu_launch_knobs.py \
+                tests/test_gpu_zerocopy.py \
                 -m gpu -x -q --timeout 120 --timeout-method thread ;;
         smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) run bench 400 python bench.py ;;
@@ -85,6 +86,13 @@ for step in "$@"; do
                 set -- $a
                 run "zc_$1_$2_q$3" 300 python3 tools/zc_stress.py --fam $1 --cs $2 --queue $3 --iters ${ZC_ITERS:-3000}
                 grep -h '^{' "$OUT/zc_$1_$2_q$3.log" >> "$OUT/zc_stress.jsonl"
+            done ;;
+        zcchurn)  # the zero-copy test's sequence on a fresh slab per iteration, beside other GPU work (tools/zc_churn.py)
+            for bg in ${ZC_BG:-none all}; do
+                for fam in ${ZC_FAMS:-rs cauchy}; do
+                    run "zcchurn_${fam}_$bg" 300 python3 -u tools/zc_churn.py --fam $fam --bg $bg --iters ${ZC_ITERS:-1500}
+                    grep -h '^{' "$OUT/zcchurn_${fam}_$bg.log" >> "$OUT/zc_churn.jsonl"
+                done
             done ;;
         tsan)  # host-TSan build (tools/tsan_build.sh, built beforehand): concurrent callers
             export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 exitcode=0 suppressions=$PWD/tools/tsan_suppressions.txt"
