@@ -79,7 +79,7 @@
 extern "C" {
 #endif
 
-#define MEC_ABI_VERSION 5
+#define MEC_ABI_VERSION 6
 #define MEC_MAX_CHUNKS 32 /* k + m <= 32: RS_N_MAX / CRS_N_MAX (rscoding.hh:5, cauchycoding.hh:5) */
 
 typedef enum {
@@ -305,6 +305,27 @@ int mec_decode_batch(mec_ctx *ctx, uint8_t *const *chunks, const uint64_t *prese
 int mec_encode_update_batch(mec_ctx *ctx, const uint32_t *data_index, const uint8_t *const *delta,
                             uint8_t *const *parity, uint32_t n_stripes, uint32_t parity_mask, int mem_kind,
                             void *stream);
+
+/* ---- pointer batches as 32-bit slab offsets (device memory; ABI 6) -------
+ *
+ * The same batches as mec_encode_batch / mec_decode_batch /
+ * mec_encode_update_batch with MEC_MEM_DEVICE, for chunks that live in one
+ * device slab (a ChunkPool-like slab, chunk_pool.cc:22-55): chunk = base +
+ * ((uint64_t)off << unit_shift), off == MEC_NULL_OFF is NULL (the
+ * Coding::zeros source / an unwanted output / a skipped delta), unit_shift
+ * <= 12 (3: 8-byte units, a 32 GiB slab; MemEC's chunk data is 8-byte
+ * aligned).  The offset rows cross PCIe at half the size of pointer rows and
+ * are expanded to pointers on the device before the coding launch; results
+ * equal the pointer-row calls' bit for bit.  Work is enqueued on `stream`;
+ * the offset arrays are consumed before return. */
+#define MEC_NULL_OFF 0xFFFFFFFFu
+int mec_encode_batch32(mec_ctx *ctx, uint8_t *base, uint32_t unit_shift, const uint32_t *data_off,
+                       const uint32_t *parity_off, uint32_t n_stripes, uint32_t parity_mask, void *stream);
+int mec_decode_batch32(mec_ctx *ctx, uint8_t *base, uint32_t unit_shift, const uint32_t *chunk_off,
+                       const uint64_t *present_masks, uint32_t n_stripes, int32_t *results, void *stream);
+int mec_encode_update_batch32(mec_ctx *ctx, uint8_t *base, uint32_t unit_shift, const uint32_t *data_index,
+                              const uint32_t *delta_off, const uint32_t *parity_off, uint32_t n_stripes,
+                              uint32_t parity_mask, void *stream);
 
 /* Coalesce concurrent mec_encode_host / mec_decode_host /
  * mec_encode_update_host calls on this context: while one batch runs,

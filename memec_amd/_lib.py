@@ -23,7 +23,9 @@ SYMBOLS = (
     "mec_encode_update_host", "mec_encode_host_batch", "mec_host_register", "mec_host_unregister",
     "mec_encode_batch", "mec_decode_batch", "mec_encode_update_batch", "mec_set_coalescing", "mec_set_host_queue", "mec_get_stats",
     "mec_set_probe", "mec_set_knob", "mec_queue_trace_enable", "mec_queue_last_trace",
+    "mec_encode_batch32", "mec_decode_batch32", "mec_encode_update_batch32",
 )
+NULL_OFF = 0xFFFFFFFF  # MEC_NULL_OFF
 MEM_DEVICE, MEM_HOST = 0, 1
 
 
@@ -93,6 +95,10 @@ def lib():
     L.mec_decode_batch.argtypes = [vp, pvp, ctypes.POINTER(u64), u32, ctypes.POINTER(ctypes.c_int32),
                                    ctypes.c_int, vp]
     L.mec_encode_update_batch.argtypes = [vp, ctypes.POINTER(u32), pvp, pvp, u32, u32, ctypes.c_int, vp]
+    pu32 = ctypes.POINTER(u32)
+    L.mec_encode_batch32.argtypes = [vp, vp, u32, pu32, pu32, u32, u32, vp]
+    L.mec_decode_batch32.argtypes = [vp, vp, u32, pu32, ctypes.POINTER(u64), u32, ctypes.POINTER(ctypes.c_int32), vp]
+    L.mec_encode_update_batch32.argtypes = [vp, vp, u32, pu32, pu32, pu32, u32, u32, vp]
     L.mec_set_coalescing.argtypes = [vp, u32]
     L.mec_set_host_queue.argtypes = [vp, u32]
     L.mec_get_stats.argtypes = [vp, ctypes.POINTER(MecStats)]

@@ -190,6 +190,50 @@ class Codec:
         check(lib().mec_encode_update_batch(self._h, di, dp, pp, n, parity_mask, self._mem(mem),
                                             self._stream_for(mem, stream)))
 
+    # ---- pointer batches as 32-bit slab offsets (device memory, ABI 6) -------------
+    # base: device address of the slab (int or CUDA tensor); offsets in units
+    # of 1 << unit_shift bytes, _lib.NULL_OFF = NULL.
+    @staticmethod
+    def _u32_array(vals):
+        a = np.ascontiguousarray(np.asarray(vals, dtype=np.uint32))
+        return ctypes.cast(a.ctypes.data, ctypes.POINTER(_lib.u32)), a
+
+    @staticmethod
+    def _base(base):
+        return vp(base.data_ptr() if hasattr(base, "data_ptr") else int(base))
+
+    def encode_batch32(self, base, unit_shift, data_off, parity_off, parity_mask=0, stream=None):
+        n = len(data_off) // self.k
+        if len(data_off) != n * self.k or len(parity_off) != n * self.m:
+            raise ValueError("need n*k data and n*m parity offsets")
+        d, _a = self._u32_array(data_off)
+        p, _b = self._u32_array(parity_off)
+        check(lib().mec_encode_batch32(self._h, self._base(base), unit_shift, d, p, n, parity_mask, _stream(stream)))
+
+    def decode_batch32(self, base, unit_shift, chunk_off, present_masks, stream=None):
+        n = len(present_masks)
+        if len(chunk_off) != n * (self.k + self.m):
+            raise ValueError("need n*(k+m) chunk offsets")
+        o, _a = self._u32_array(chunk_off)
+        pmv = np.ascontiguousarray(np.asarray(present_masks, dtype=np.uint64))
+        pm = ctypes.cast(pmv.ctypes.data, ctypes.POINTER(_lib.u64))
+        res = (ctypes.c_int32 * n)()
+        rc = lib().mec_decode_batch32(self._h, self._base(base), unit_shift, o, pm, n, res, _stream(stream))
+        out = list(res)
+        if rc < 0 and rc not in out:
+            check(rc)
+        return out
+
+    def encode_update_batch32(self, base, unit_shift, data_index, delta_off, parity_off, parity_mask=0, stream=None):
+        n = len(data_index)
+        if len(delta_off) != n or len(parity_off) != n * self.m:
+            raise ValueError("need n deltas and n*m parity offsets")
+        di, _a = self._u32_array(data_index)
+        d, _b = self._u32_array(delta_off)
+        p, _c = self._u32_array(parity_off)
+        check(lib().mec_encode_update_batch32(self._h, self._base(base), unit_shift, di, d, p, n, parity_mask,
+                                              _stream(stream)))
+
     def set_coalescing(self, max_batch):
         check(lib().mec_set_coalescing(self._h, max_batch))
 

@@ -307,9 +307,29 @@ uint8_t gather_shape(const void *tab, uint32_t stride, uint32_t n) {
     return (bits & 127) ? 2 : 1;
 }
 
+// 32-bit slab offset rows (mec_*_batch32): entry = base + (off << shift),
+// kNullOff = NULL.  The rows cross PCIe at half the size of pointer rows and
+// are expanded to pointers on the device (launch_expand_rows), so every
+// gathered kernel reads the same pointer table as for mec_*_batch.
+struct Off32 {
+    uint64_t base;
+    uint32_t shift;
+};
+constexpr uint32_t kMaxOffShift = 12;
+
+uint8_t gather_shape32(const uint32_t *tab, uint32_t stride, uint32_t n, const Off32 &o) {
+    uint64_t bits = 0;
+    const size_t cnt = size_t(std::min<uint32_t>(n, 64)) * stride;
+    for (size_t i = 0; i < cnt; ++i)
+        if (tab[i] != kNullOff) bits |= o.base + (uint64_t(tab[i]) << o.shift);
+    return (bits & 127) ? 2 : 1;
+}
+
 int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, const void *dtab, uint32_t dstride,
-               const uint16_t *pat, uint32_t n, hipStream_t st, bool mapped_tables = false, bool device_mem = true) {
+               const uint16_t *pat, uint32_t n, hipStream_t st, bool mapped_tables = false, bool device_mem = true,
+               const Off32 *o32 = nullptr) {
     if (M.ssel.empty() || M.rows() == 0 || n == 0) return MEC_OK;
+    const size_t es = o32 ? 4 : 8;  // bytes per row entry on the host
     // a single map with no skipped stripe runs from kernel arguments;
     // anything else through per-stripe descriptors (and byte-wise maps with
     // more than 4 outputs too: the descriptor kernel codes every row group
@@ -329,8 +349,8 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
     const size_t groups = single ? 0 : build_descs(c, M, descs, desc_dw);
     const bool same = stab == dtab && sstride == dstride;
     std::vector<std::pair<const void *, size_t>> parts = {
-        {stab, size_t(n) * sstride * 8},
-        {same ? nullptr : dtab, same ? 0 : size_t(n) * dstride * 8},
+        {stab, size_t(n) * sstride * es},
+        {same ? nullptr : dtab, same ? 0 : size_t(n) * dstride * es},
         {single ? nullptr : pat, (pat && !single) ? size_t(n) * 2 : 0},
         {descs.data(), descs.size() * sizeof(uint32_t)}};
     SlotHold hold;
@@ -341,6 +361,32 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
     if (rc != MEC_OK) return rc;
     const uint64_t *dstab = reinterpret_cast<const uint64_t *>(dev + offs[0]);
     const uint64_t *ddtab = reinterpret_cast<const uint64_t *>(dev + offs[same ? 0 : 1]);
+    if (o32) {  // expand the offset rows into the slot's pointer table, on st after the copy
+        TableSlot &t = *hold.t;
+        const size_t ne_s = size_t(n) * sstride, ne_d = same ? 0 : size_t(n) * dstride;
+        const size_t need = (ne_s + ne_d) * 8;
+        if (t.xcap < need) {
+            if (t.xdev) (void)hipFree(t.xdev);
+            t.xdev = nullptr;
+            t.xcap = 0;
+            HIP_TRY(hipMalloc(reinterpret_cast<void **>(&t.xdev), std::max<size_t>(need, size_t(1) << 20)));
+            t.xcap = std::max<size_t>(need, size_t(1) << 20);
+        }
+        HIP_TRY(launch_expand_rows(reinterpret_cast<const uint32_t *>(dev + offs[0]), t.xdev, o32->base, o32->shift,
+                                   ne_s, st));
+        if (!same)
+            HIP_TRY(launch_expand_rows(reinterpret_cast<const uint32_t *>(dev + offs[1]), t.xdev + ne_s, o32->base,
+                                       o32->shift, ne_d, st));
+        dstab = t.xdev;
+        ddtab = same ? t.xdev : t.xdev + ne_s;
+    }
+    auto shape_of = [&]() -> uint8_t {
+        if (!device_mem) return 0;
+        if (o32)
+            return std::max(gather_shape32(static_cast<const uint32_t *>(stab), sstride, n, *o32),
+                            gather_shape32(static_cast<const uint32_t *>(dtab), dstride, n, *o32));
+        return std::max(gather_shape(stab, sstride, n), gather_shape(dtab, dstride, n));
+    };
     const size_t rows = M.rows(), nm = M.ssel.size();
     if (single) {
         // one map for every stripe: the map goes in kernel arguments
@@ -399,7 +445,7 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
                 L.len = c->cs;
                 L.n_stripes = n;
                 L.accumulate = M.accumulate;
-                L.gshape = device_mem ? std::max(gather_shape(stab, sstride, n), gather_shape(dtab, dstride, n)) : 0;
+                L.gshape = shape_of();
                 for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
                 for (int i = 0; i < nr; ++i) {
                     L.dst_off[i] = ds[r0 + i];
@@ -419,7 +465,7 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
                 L.packet = c->packet;
                 L.n_stripes = n;
                 L.accumulate = M.accumulate;
-                L.gshape = device_mem ? std::max(gather_shape(stab, sstride, n), gather_shape(dtab, dstride, n)) : 0;
+                L.gshape = shape_of();
                 for (uint32_t j = 0; j < M.K; ++j) L.src_off[j] = ss[j];
                 for (int i = 0; i < nr; ++i) {
                     L.dst_off[i] = ds[r0 + i];
@@ -764,6 +810,7 @@ void batch_release(mec_ctx *c) {
         if (t.copied) (void)hipEventDestroy(t.copied);
         if (t.host) (void)hipHostFree(t.host);
         if (t.dev) (void)hipFree(t.dev);
+        if (t.xdev) (void)hipFree(t.xdev);
     }
     if (c->tab_stream) {
         (void)hipStreamSynchronize(c->tab_stream);
@@ -777,6 +824,57 @@ void batch_release(mec_ctx *c) {
         }
         if (P.done[b]) (void)hipEventDestroy(P.done[b]);
         if (P.host[b]) (void)hipHostFree(P.host[b]);
+    }
+}
+
+// The maps of a device decode batch: one per distinct erasure pattern
+// (cached plans), pat[s] its index or kSkipStripe (nothing missing, or the
+// stripe failed: its status goes to note(s, rc)).  is_null(s, i): chunk i
+// of stripe s is NULL.
+template <typename IsNull, typename Note>
+void decode_maps(mec_ctx *c, const uint64_t *present_masks, uint32_t n_stripes, IsNull is_null, MapSet &M,
+                 std::vector<uint16_t> &pat, Note note) {
+    const uint32_t n = c->k + c->m;
+    const uint64_t full = (uint64_t(1) << n) - 1;
+    M.K = c->k;
+    pat.assign(n_stripes, kSkipStripe);
+    std::unordered_map<uint64_t, uint16_t> ids;
+    uint64_t last_mask = ~uint64_t(0);
+    uint16_t last_id = kSkipStripe;
+    for (uint32_t s = 0; s < n_stripes; ++s) {
+        const uint64_t present = present_masks[s] & full;
+        int src = MEC_OK;
+        const uint32_t failed = uint32_t(__builtin_popcountll(~present & full));
+        if (failed > c->m) {
+            src = fail(MEC_ETOOMANY, "Too many failure to recover (%u>%u)", failed, c->m);
+        } else if (failed > 0) {
+            for (uint32_t i = 0; i < n && src == MEC_OK; ++i)
+                if (is_null(s, i)) src = fail(MEC_EINVAL, "chunk %u pointer is NULL", i);
+            if (src == MEC_OK) {
+                if (present != last_mask) {
+                    auto it = ids.find(present);
+                    if (it == ids.end()) {
+                        const LinearPlan *plan = nullptr;
+                        src = get_plan(c, present, plan);
+                        if (src == MEC_OK) {
+                            if (M.ssel.size() >= kSkipStripe) {
+                                src = fail(MEC_EINVAL, "too many distinct erasure patterns in one batch");
+                            } else {
+                                std::vector<uint8_t> ss(plan->src.begin(), plan->src.end());
+                                std::vector<uint8_t> ds(plan->dst.begin(), plan->dst.end());
+                                it = ids.emplace(present, uint16_t(M.add(ss, ds, plan->coef))).first;
+                            }
+                        }
+                    }
+                    if (src == MEC_OK) {
+                        last_mask = present;
+                        last_id = it->second;
+                    }
+                }
+                if (src == MEC_OK) pat[s] = last_id;
+            }
+        }
+        note(s, src);
     }
 }
 
@@ -861,7 +959,6 @@ int mec_decode_batch(mec_ctx *c, uint8_t *const *chunks, const uint64_t *present
     int first = MEC_OK;
     std::string first_err;
     const uint32_t n = c->k + c->m;
-    const uint64_t full = (uint64_t(1) << n) - 1;
     auto note = [&](uint32_t s, int rc) {
         if (results) results[s] = rc;
         if (rc != MEC_OK && first == MEC_OK) {
@@ -873,47 +970,9 @@ int mec_decode_batch(mec_ctx *c, uint8_t *const *chunks, const uint64_t *present
     int rc = MEC_OK;
     if (mem_kind == MEC_MEM_DEVICE) {
         MapSet M;
-        M.K = c->k;
-        std::vector<uint16_t> pat(n_stripes, kSkipStripe);
-        std::unordered_map<uint64_t, uint16_t> ids;
-        uint64_t last_mask = ~uint64_t(0);
-        uint16_t last_id = kSkipStripe;
-        for (uint32_t s = 0; s < n_stripes; ++s) {
-            const uint64_t present = present_masks[s] & full;
-            uint8_t *const *row = chunks + size_t(s) * n;
-            int src = MEC_OK;
-            const uint32_t failed = uint32_t(__builtin_popcountll(~present & full));
-            if (failed > c->m) {
-                src = fail(MEC_ETOOMANY, "Too many failure to recover (%u>%u)", failed, c->m);
-            } else if (failed > 0) {
-                for (uint32_t i = 0; i < n && src == MEC_OK; ++i)
-                    if (!row[i]) src = fail(MEC_EINVAL, "chunk %u pointer is NULL", i);
-                if (src == MEC_OK) {
-                    if (present != last_mask) {
-                        auto it = ids.find(present);
-                        if (it == ids.end()) {
-                            const LinearPlan *plan = nullptr;
-                            src = get_plan(c, present, plan);
-                            if (src == MEC_OK) {
-                                if (M.ssel.size() >= kSkipStripe) {
-                                    src = fail(MEC_EINVAL, "too many distinct erasure patterns in one batch");
-                                } else {
-                                    std::vector<uint8_t> ss(plan->src.begin(), plan->src.end());
-                                    std::vector<uint8_t> ds(plan->dst.begin(), plan->dst.end());
-                                    it = ids.emplace(present, uint16_t(M.add(ss, ds, plan->coef))).first;
-                                }
-                            }
-                        }
-                        if (src == MEC_OK) {
-                            last_mask = present;
-                            last_id = it->second;
-                        }
-                    }
-                    if (src == MEC_OK) pat[s] = last_id;
-                }
-            }
-            note(s, src);
-        }
+        std::vector<uint16_t> pat;
+        decode_maps(c, present_masks, n_stripes, [&](uint32_t s, uint32_t i) { return !chunks[size_t(s) * n + i]; }, M,
+                    pat, note);
         rc = run_gather(c, M, chunks, n, chunks, n, pat.data(), n_stripes, hipStream_t(stream));
     } else {
         GroupSet G;
@@ -973,6 +1032,95 @@ int mec_encode_update_batch(mec_ctx *c, const uint32_t *data_index, const uint8_
         add_update(c, G, data_index[s], delta[s], parity + size_t(s) * c->m, pm, int32_t(s));
     }
     return run_host(c, G.groups);
+}
+
+// ---- 32-bit slab offsets (device memory) ----------------------------------
+
+#define MEC_CHECK_OFF32(c, base, shift)                                                        \
+    do {                                                                                        \
+        if (!(base)) return fail(MEC_EINVAL, "null slab base");                                \
+        if ((shift) > kMaxOffShift) return fail(MEC_EINVAL, "unit_shift %u > %u", (shift), kMaxOffShift); \
+    } while (0)
+
+int mec_encode_batch32(mec_ctx *c, uint8_t *base, uint32_t unit_shift, const uint32_t *data_off,
+                       const uint32_t *parity_off, uint32_t n_stripes, uint32_t parity_mask, void *stream) {
+    CHECK_CTX(c);
+    if (n_stripes == 0) return MEC_OK;
+    MEC_CHECK_OFF32(c, base, unit_shift);
+    if (!data_off || !parity_off) return fail(MEC_EINVAL, "null offset array");
+    const uint32_t pm = parity_mask ? parity_mask : full_mask32(c->m);
+    DeviceGuard dg(c->device);
+    MapSet M;
+    M.K = c->k;
+    std::vector<uint32_t> rows = bits_of(pm, c->m), cols = bits_of(full_mask32(c->k), c->k);
+    std::vector<uint8_t> ss(cols.begin(), cols.end()), ds(rows.begin(), rows.end());
+    M.add(ss, ds, encode_rows(c, rows, cols));
+    const Off32 o{uint64_t(uintptr_t(base)), unit_shift};
+    return run_gather(c, M, data_off, c->k, parity_off, c->m, nullptr, n_stripes, hipStream_t(stream), false, true, &o);
+}
+
+int mec_decode_batch32(mec_ctx *c, uint8_t *base, uint32_t unit_shift, const uint32_t *chunk_off,
+                       const uint64_t *present_masks, uint32_t n_stripes, int32_t *results, void *stream) {
+    CHECK_CTX(c);
+    if (n_stripes == 0) return MEC_OK;
+    MEC_CHECK_OFF32(c, base, unit_shift);
+    if (!chunk_off || !present_masks) return fail(MEC_EINVAL, "null offset array");
+    int first = MEC_OK;
+    std::string first_err;
+    const uint32_t n = c->k + c->m;
+    auto note = [&](uint32_t s, int rc) {
+        if (results) results[s] = rc;
+        if (rc != MEC_OK && first == MEC_OK) {
+            first = rc;
+            first_err = "stripe " + std::to_string(s) + ": " + g_err;
+        }
+    };
+    DeviceGuard dg(c->device);
+    MapSet M;
+    std::vector<uint16_t> pat;
+    decode_maps(c, present_masks, n_stripes,
+                [&](uint32_t s, uint32_t i) { return chunk_off[size_t(s) * n + i] == kNullOff; }, M, pat, note);
+    const Off32 o{uint64_t(uintptr_t(base)), unit_shift};
+    const int rc = run_gather(c, M, chunk_off, n, chunk_off, n, pat.data(), n_stripes, hipStream_t(stream), false, true, &o);
+    if (rc != MEC_OK) {
+        if (results)
+            for (uint32_t s = 0; s < n_stripes; ++s)
+                if (results[s] == MEC_OK) results[s] = rc;
+        return rc;
+    }
+    if (first != MEC_OK) g_err = first_err;
+    return first;
+}
+
+int mec_encode_update_batch32(mec_ctx *c, uint8_t *base, uint32_t unit_shift, const uint32_t *data_index,
+                              const uint32_t *delta_off, const uint32_t *parity_off, uint32_t n_stripes,
+                              uint32_t parity_mask, void *stream) {
+    CHECK_CTX(c);
+    if (n_stripes == 0) return MEC_OK;
+    MEC_CHECK_OFF32(c, base, unit_shift);
+    if (!data_index || !delta_off || !parity_off) return fail(MEC_EINVAL, "null offset array");
+    for (uint32_t s = 0; s < n_stripes; ++s)
+        if (data_index[s] >= c->k) return fail(MEC_EINVAL, "stripe %u: data_index %u >= k %u", s, data_index[s], c->k);
+    const uint32_t pm = parity_mask ? parity_mask : full_mask32(c->m);
+    DeviceGuard dg(c->device);
+    MapSet M;
+    M.K = 1;
+    M.accumulate = true;
+    const std::vector<uint32_t> rows = bits_of(pm, c->m);
+    const std::vector<uint8_t> ds(rows.begin(), rows.end());
+    std::vector<int> id_of(c->k, -1);
+    std::vector<uint16_t> pat(n_stripes);
+    for (uint32_t s = 0; s < n_stripes; ++s) {
+        if (delta_off[s] == kNullOff) {
+            pat[s] = kSkipStripe;
+            continue;
+        }
+        const uint32_t j = data_index[s];
+        if (id_of[j] < 0) id_of[j] = int(M.add({0}, ds, encode_rows(c, rows, {j})));
+        pat[s] = uint16_t(id_of[j]);
+    }
+    const Off32 o{uint64_t(uintptr_t(base)), unit_shift};
+    return run_gather(c, M, delta_off, 1, parity_off, c->m, pat.data(), n_stripes, hipStream_t(stream), false, true, &o);
 }
 
 int mec_set_coalescing(mec_ctx *c, uint32_t max_batch) {

@@ -78,6 +78,8 @@ struct TableSlot {
     hipEvent_t done = nullptr;    // the launches that read dev have finished (on the caller's stream)
     hipEvent_t copied = nullptr;  // dev holds this call's tables (on the context's copy stream)
     bool pending = false;
+    uint64_t *xdev = nullptr;  // 32-bit slab offset rows expanded to pointers (mec_*_batch32)
+    size_t xcap = 0;           // bytes
 };
 constexpr int kTableSlots = 4;
 

@@ -413,6 +413,31 @@ hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t
     return hipGetLastError();
 }
 
+// 32-bit slab offsets -> chunk pointers (mec_*_batch32): entry e becomes
+// base + (off << shift), or 0 (NULL) for kNullOff.  Four entries per lane:
+// one 16-byte load, two 16-byte stores; the rest one at a time.
+__global__ __launch_bounds__(kThreads) void expand_rows_kernel(const uint32_t *in, uint64_t *out, uint64_t base,
+                                                               uint32_t shift, uint64_t n) {
+    const uint64_t q = uint64_t(blockIdx.x) * kThreads + threadIdx.x, e = q * 4;
+    auto one = [&](uint32_t o) -> uint64_t { return o == kNullOff ? 0 : base + (uint64_t(o) << shift); };
+    if (e + 4 <= n) {
+        const u32x4 v = *reinterpret_cast<const u32x4 *>(in + e);
+        reinterpret_cast<u64x2 *>(out + e)[0] = u64x2{one(v.x), one(v.y)};
+        reinterpret_cast<u64x2 *>(out + e)[1] = u64x2{one(v.z), one(v.w)};
+    } else {
+        for (uint64_t i = e; i < n; ++i) out[i] = one(in[i]);
+    }
+}
+
+hipError_t launch_expand_rows(const uint32_t *in, uint64_t *out, uint64_t base, uint32_t shift, uint64_t n,
+                              hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n + 4ull * kThreads - 1) / (4ull * kThreads);
+    if (blocks >= (uint64_t(1) << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(expand_rows_kernel, dim3(uint32_t(blocks)), dim3(kThreads), 0, stream, in, out, base, shift, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_fill(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_offset, hipStream_t stream) {
     if (len == 0) return hipSuccess;
     hipLaunchKernelGGL(fill_kernel, dim3(stream_blocks(len)), dim3(kThreads), 0, stream, dst, len, seed,

@@ -174,5 +174,11 @@ hipError_t launch_bm_gather(const GatherLaunch &L, hipStream_t stream);
 hipError_t launch_bm(const BmLaunch &L, hipStream_t stream);
 hipError_t launch_xor(uint8_t *dst, const uint8_t *a, const uint8_t *b, uint64_t len, hipStream_t stream);
 hipError_t launch_fill(uint8_t *dst, uint64_t len, uint64_t seed, uint64_t word_offset, hipStream_t stream);
+// 32-bit slab offsets (mec_*_batch32) expanded into chunk pointers on the
+// device: out[e] = in[e] == kNullOff ? 0 : base + (in[e] << shift).  in must
+// be 16-byte aligned.
+constexpr uint32_t kNullOff = 0xFFFFFFFFu;
+hipError_t launch_expand_rows(const uint32_t *in, uint64_t *out, uint64_t base, uint32_t shift, uint64_t n,
+                              hipStream_t stream);
 
 }  // namespace mec

@@ -30,6 +30,7 @@ namespace detail {
 #endif
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 // Streamed-once data: non-temporal loads/stores keep the stripe bytes from

@@ -115,6 +115,155 @@ def ref_delta(scheme, k, m, cs, seed, col, index):
     return out
 
 
+def isal_decode_case(fam, k, m, cs, pat, s):
+    """The USE_ISAL plugin's decode of a random non-codeword stripe (as the
+    ISA-L section of main()): (ok, out, fixed, defect).  Erased data chunks
+    are the plugin's bytes; erased parity chunks are zeros in `out` (the
+    plugin reads them from uninitialised stack, rscoding.cc:173-175) and the
+    plugin's own encode of the decoded data in `fixed`."""
+    chunks = fill((k + m) * cs, s)
+    present = sum(1 << i for i in range(k + m) if i not in pat)
+    outs, rcs = [], []
+    for poison in (0x00, 0xA5):
+        work = chunks.copy()
+        for e in pat:
+            work[e * cs:(e + 1) * cs] = 0
+        h = ctypes.c_void_p(REFI.refi_instantiate(ISAL_SCHEME[fam], k, m, cs))
+        rcs.append(REFI.refi_decode_poisoned(h, ptr(work), ctypes.c_uint64(present), poison))
+        REFI.refi_destroy(h)
+        outs.append(work)
+    assert rcs[0] == rcs[1], (fam, k, m, pat)
+    if rcs[1] != 0:
+        return False, None, None, None
+    work = outs[1]
+    out = np.concatenate([work[e * cs:(e + 1) * cs] for e in sorted(pat)])
+    for e in pat:
+        if e < k:
+            assert np.array_equal(outs[0][e * cs:(e + 1) * cs], work[e * cs:(e + 1) * cs]), (fam, pat)
+    fixed = out.copy()
+    defect = []
+    for r, e in enumerate(sorted(pat)):
+        if e < k:
+            continue
+        par = np.zeros(cs, np.uint8)
+        refi_encode(fam, k, m, cs, work[:k * cs].copy(), par, e - k + 1)
+        fixed[r * cs:(r + 1) * cs] = par
+        defect.append(bool(not np.array_equal(out[r * cs:(r + 1) * cs], par)))
+        out[r * cs:(r + 1) * cs] = 0
+    return True, out, fixed, defect
+
+
+def wide_cases(meta, blobs, seed):
+    """Round 6: wide codes pinned on the reference itself
+    — more than 4 parities, decodes of 5..8 erasures — where the engine runs
+    its bit-sliced and one-pass kernels.  Jerasure RS /
+    Cauchy through libmemec_ref.so (jerasure.c:167-268, cauchycoding.cc:87-180),
+    ISA-L RS / Cauchy through the USE_ISAL plugin (rscoding.cc:155-177).
+    Chunk sizes include ones that are not a multiple of the bit-sliced
+    kernels' 2 KiB tile."""
+    # Jerasure encodes, m > 4
+    for idx, (fam, k, m, cs, n) in enumerate([("rs", 16, 8, 2560, 1), ("rs", 12, 8, 1024, 2), ("rs", 10, 6, 2048, 1),
+                                              ("rs", 4, 12, 512, 1), ("cauchy", 10, 6, 2560, 1),
+                                              ("cauchy", 16, 8, 1024, 1), ("cauchy", 8, 5, 1280, 1)]):
+        scheme = CS_RS if fam == "rs" else CS_CAUCHY
+        s = seed + 6000 + idx
+        _, par = ref_encode_stripes(scheme, k, m, cs, n, s)
+        name = "enc/%s/%d_%d_%d_x%d" % (fam, k, m, cs, n)
+        assert name not in meta["cases"], name
+        blobs[name] = par
+        meta["cases"][name] = {"kind": "encode", "family": fam, "k": k, "m": m, "chunk": cs, "stripes": n, "seed": s,
+                               "w": ref_getw(scheme, k, m, cs), "wide": True,
+                               "data_layout": "[stripe][k][chunk] from one splitmix stream",
+                               "parity_layout": "[stripe][m][chunk]"}
+    # Jerasure decodes of random non-codeword stripes, 5..8 erasures
+    jdec = [
+        ("rs", 16, 8, 2560, [[0, 1, 2, 3, 4], [0, 2, 4, 6, 8, 10], [1, 3, 5, 7, 9, 11, 13], [0, 1, 2, 3, 4, 5, 6, 7],
+                             [3, 7, 11, 15, 16, 18, 20, 22], [16, 17, 18, 19, 20, 21, 22, 23], [0, 5, 9, 13, 17, 21, 23],
+                             [8, 9, 10, 11, 12, 16, 17, 18], [15, 16]]),
+        ("rs", 12, 8, 1024, [[0, 1, 2, 3, 4, 5], [0, 12, 13, 14, 15, 16, 17, 18], [11, 12, 19], [2, 4, 6, 8, 10, 13, 15]]),
+        ("cauchy", 10, 6, 2560, [[0, 1, 2, 3, 4], [0, 1, 2, 3, 4, 5], [0, 3, 6, 9, 10, 15], [10, 11, 12, 13, 14, 15],
+                                 [1, 4, 7, 11, 13]]),
+        ("cauchy", 16, 8, 1024, [[0, 1, 2, 3, 4, 5, 6, 7], [2, 5, 8, 11, 16, 19, 22, 23], [16, 17, 18, 19, 20]]),
+    ]
+    for idx, (fam, k, m, cs, pats) in enumerate(jdec):
+        scheme = CS_RS if fam == "rs" else CS_CAUCHY
+        for p_i, pat in enumerate(pats):
+            s = seed + 8000 + 100 * idx + p_i
+            rc, out = ref_decode_random(scheme, k, m, cs, s, pat)
+            assert rc == 0, (fam, k, m, pat)
+            name = "dec/%s/%d_%d_%d/%s" % (fam, k, m, cs, "-".join(map(str, pat)))
+            blobs[name] = out
+            meta["cases"][name] = {"kind": "decode_random", "family": fam, "k": k, "m": m, "chunk": cs,
+                                   "seed": s, "erased": pat, "rc": rc, "w": ref_getw(scheme, k, m, cs), "wide": True,
+                                   "input_layout": "[k+m][chunk] random; erased chunks cleared before decode",
+                                   "output_layout": "erased chunks ascending"}
+    # ISA-L encodes and offset updates, m > 4 (ec_encode_data_base through the plugin)
+    for (k, m, cs) in [(12, 8, 1024), (12, 6, 2560), (4, 12, 512)]:
+        for fam, gen in (("isal_rs", REF.ref_isal_gen_rs_matrix), ("isal_cauchy", REF.ref_isal_gen_cauchy1_matrix)):
+            a = np.zeros((k + m) * k, dtype=np.uint8)
+            gen(ptr(a), k + m, k)
+            meta["isal_matrices"]["%s/%d,%d" % (fam, k, m)] = a.tolist()
+            s = seed + 9000 + k * 100 + m + (0 if fam == "isal_rs" else 50)
+            data = fill(k * cs, s)
+            par = np.zeros(m * cs, dtype=np.uint8)
+            for i in range(m):
+                one = np.zeros(cs, dtype=np.uint8)
+                refi_encode(fam, k, m, cs, data, one, i + 1)
+                par[i * cs:(i + 1) * cs] = one
+            chk = np.zeros(m * cs, dtype=np.uint8)
+            src = (u8p * k)(*[ptr(data[j * cs:]) for j in range(k)])
+            dst = (u8p * m)(*[ptr(chk[i * cs:]) for i in range(m)])
+            REF.ref_isal_encode(cs, k, m, ptr(a[k * k:].copy()), src, dst)
+            assert np.array_equal(par, chk), (fam, k, m)
+            name = "enc/%s/%d_%d_%d_x1" % (fam, k, m, cs)
+            blobs[name] = par
+            meta["cases"][name] = {"kind": "encode", "family": fam, "k": k, "m": m, "chunk": cs, "stripes": 1,
+                                   "seed": s, "wide": True, "data_layout": "[k][chunk]", "parity_layout": "[m][chunk]"}
+            # the server's delta call: encode(data, parity, index, startOff, endOff)
+            for j, (index, st, ed) in enumerate([(m, 1 * cs + 5, (k - 1) * cs + 1), (m - 2, (k - 1) * cs, k * cs)]):
+                s2 = seed + 9500 + k * 100 + m * 4 + j + (0 if fam == "isal_rs" else 50)
+                d2 = fill(k * cs, s2)
+                p2 = fill(cs, s2 + 1)
+                refi_encode(fam, k, m, cs, d2, p2, index, st, ed)
+                name = "encoff/%s/%d_%d_%d/i%d_s%d_e%d" % (fam, k, m, cs, index, st, ed)
+                blobs[name] = p2
+                meta["cases"][name] = {"kind": "encode_offsets_isal", "family": fam, "k": k, "m": m, "chunk": cs,
+                                       "seed": s2, "parity_seed": s2 + 1, "index": index, "startOff": st, "endOff": ed,
+                                       "wide": True, "data_layout": "[k][chunk] splitmix(seed)",
+                                       "parity_in": "[chunk] splitmix(parity_seed), the caller's parity chunk",
+                                       "expected": "the caller's parity chunk after the reference plugin's "
+                                                   "RSCoding/CauchyCoding::encode (USE_ISAL)"}
+    # ISA-L decodes of random non-codeword stripes, 5..8 erasures: data-only
+    # patterns (the plugin's own bytes) and mixed ones (`fixed` for parity)
+    idec = [(12, 8, 1024, [[0, 1, 2, 3, 4], [0, 2, 4, 6, 8, 10], [0, 1, 2, 3, 4, 5, 6], [4, 5, 6, 7, 8, 9, 10, 11],
+                           [0, 1, 2, 3, 5, 7, 9, 11], [1, 3, 5, 12, 14, 16, 18], [12, 13, 14, 15, 16, 17, 18, 19],
+                           # singular for ISA-L RS (gf_gen_rs_matrix is not MDS at this size: the
+                           # plugin's gf_invert_matrix fails, decode() returns false); Cauchy decodes it
+                           [0, 1, 2, 4, 5, 8, 12, 15]]),
+            (12, 6, 2560, [[0, 1, 2, 3, 4], [0, 1, 2, 3, 4, 5], [6, 7, 8, 9, 10, 11], [1, 3, 5, 7, 9, 11],
+                           [0, 11, 12, 14, 16, 17]])]
+    for fam_i, fam in enumerate(("isal_rs", "isal_cauchy")):
+        for idx, (k, m, cs, pats) in enumerate(idec):
+            for p_i, pat in enumerate(pats):
+                s = seed + 10000 + 1000 * fam_i + 100 * idx + p_i
+                ok, out, fixed, defect = isal_decode_case(fam, k, m, cs, pat, s)
+                name = "dec/%s/%d_%d_%d/%s" % (fam, k, m, cs, "-".join(map(str, pat)))
+                if not ok:  # the k x k survivor matrix is singular: the plugin returns false
+                    meta["cases"][name] = {"kind": "decode_singular_isal", "family": fam, "k": k, "m": m,
+                                           "chunk": cs, "seed": s, "erased": pat, "rc": 0, "wide": True}
+                    continue
+                blobs[name] = out
+                blobs[name + "|fixed"] = fixed
+                meta["cases"][name] = {"kind": "decode_random_isal", "family": fam, "k": k, "m": m, "chunk": cs,
+                                       "seed": s, "erased": pat, "rc": 1, "reference_parity_defect": defect,
+                                       "wide": True,
+                                       "input_layout": "[k+m][chunk] random; erased chunks cleared before decode",
+                                       "output_layout": "erased chunks ascending (reference plugin output; "
+                                                        "erased parity undefined there, zeroed)",
+                                       "fixed_layout": "same; erased parity = the reference plugin's encode "
+                                                       "of the decoded data"}
+
+
 def main():
     meta = {"generator": "tests/golden/make_golden.py",
             "reference": "mtyiu/memec common/coding over lib/jerasure + lib/gf_complete; the same plugin built USE_ISAL over ISA-L 2.14 ec_base.c + ec_highlevel_func.c",
@@ -370,6 +519,8 @@ def main():
                                    "parity_in": "[chunk] splitmix(parity_seed), the caller's parity chunk",
                                    "expected": "the caller's parity chunk after the reference plugin's "
                                                "RSCoding/CauchyCoding::encode (USE_ISAL)"}
+
+    wide_cases(meta, blobs, seed)
 
     np.savez_compressed(os.path.join(HERE, "golden.npz"), **{k.replace("/", "|"): v for k, v in blobs.items()})
     with open(os.path.join(HERE, "golden.json"), "w") as f:

@@ -26,7 +26,7 @@ def test_exports_every_declared_symbol():
     for name in declared:
         assert hasattr(L, name), name
     assert set(declared) == set(_lib.SYMBOLS)
-    assert L.mec_abi_version() == 5
+    assert L.mec_abi_version() == 6
 
 
 def test_coding_adapter_library_links():

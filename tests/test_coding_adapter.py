@@ -74,7 +74,7 @@ def test_isal_encode_offsets_match_reference(binaries, golden, tmp_path):
     overwrites with a full encode)."""
     meta, blobs = golden
     cases = [(n, c) for n, c in sorted(meta["cases"].items()) if c["kind"] == "encode_offsets_isal"]
-    assert len(cases) == 8
+    assert len(cases) >= 20  # 8 with m <= 4, 12 wide (round 6)
     isal_bin = binaries[1]
     for name, c in cases:
         out = tmp_path / "par.bin"

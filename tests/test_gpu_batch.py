@@ -473,3 +473,90 @@ def test_device_batches_from_threads_share_table_slots():
         x.join()
     c.close()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("fam", FAMS)
+@pytest.mark.parametrize("cs,shift", [(4096, 3), (1032, 3), (65536, 0)])
+def test_batch32_slab_offsets(fam, cs, shift):
+    """mec_*_batch32 (ABI 6): the pointer batches given
+    as 32-bit offsets into one device slab (ChunkPool-like slots of
+    8 + chunkSize bytes in random order, chunk_pool.cc:22-55) — encode with
+    Coding::zeros columns and unwanted parities (MEC_NULL_OFF), decode with a
+    different pattern per stripe (none, <= m, > m), delta updates with
+    skipped stripes — equal the 64-bit pointer-row calls and the oracle."""
+    k, m, n = 6, 3, 40
+    if fam == "cauchy" and O.cauchy_getw(k, m, cs) < 1:
+        pytest.skip("no Cauchy w for this chunk size")
+    NULL = _lib.NULL_OFF
+    rng = np.random.default_rng(cs + shift)
+    slab = Slab(n * (k + m), cs, 8, True, 9 + cs)
+    twin = Slab(n * (k + m), cs, 8, True, 9 + cs)
+    slots = rng.permutation(n * (k + m))
+    off = lambda i: (i * slab.slot + slab.hdr) >> shift  # noqa: E731
+    if shift:
+        assert all((i * slab.slot + slab.hdr) % (1 << shift) == 0 for i in range(4))
+    c = Codec(fam, k, m, cs)
+    # encode: column 2 of every 5th stripe is Coding::zeros, parity 1 unwanted on odd stripes
+    doff, poff, dptr, pptr = [], [], [], []
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        for j in range(k):
+            z = s % 5 == 0 and j == 2
+            doff.append(NULL if z else off(row[j]))
+            dptr.append(0 if z else twin.addr(row[j]))
+        for i in range(m):
+            u = s % 2 == 1 and i == 1
+            poff.append(NULL if u else off(row[k + i]))
+            pptr.append(0 if u else twin.addr(row[k + i]))
+    c.encode_batch32(slab.t, shift, doff, poff)
+    c.encode_batch(dptr, pptr)
+    torch.cuda.synchronize()
+    assert torch.equal(slab.t, twin.t)
+    for s in range(0, n, 7):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        data = [np.zeros(cs, np.uint8) if (s % 5 == 0 and j == 2) else slab.chunk(row[j]) for j in range(k)]
+        want = O.encode(fam, k, m, data, cs)
+        for i in range(m):
+            if not (s % 2 == 1 and i == 1):
+                assert np.array_equal(slab.chunk(row[k + i]), want[i]), (s, i)
+    # decode: per-stripe patterns, every 9th has more than m missing
+    masks, coff, cptr, pats = [], [], [], []
+    for s in range(n):
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        e = m + 1 if s % 9 == 4 else int(rng.integers(0, m + 1))
+        pat = sorted(rng.choice(k + m, size=e, replace=False).tolist())
+        pats.append(pat)
+        masks.append(sum(1 << i for i in range(k + m) if i not in pat))
+        coff += [off(x) for x in row]
+        cptr += [twin.addr(x) for x in row]
+    before = slab.t.clone()
+    r32 = c.decode_batch32(slab.t, shift, coff, masks)
+    r64 = c.decode_batch(cptr, masks)
+    assert r32 == r64
+    assert all((r == _lib.MEC_ETOOMANY) == (s % 9 == 4) for s, r in enumerate(r32))
+    torch.cuda.synchronize()
+    assert torch.equal(slab.t, twin.t)
+    hb = before.cpu().numpy()
+    for s in range(1, n, 6):
+        if len(pats[s]) > m or not pats[s]:
+            continue
+        row = slots[s * (k + m):(s + 1) * (k + m)]
+        chunks = [hb[x * slab.slot + 8:x * slab.slot + 8 + cs].copy() for x in row]
+        assert O.decode(fam, k, m, chunks, pats[s], cs) == 0
+        for i in range(k + m):
+            assert np.array_equal(slab.chunk(row[i]), chunks[i]), (s, pats[s], i)
+    # delta updates: stripe s's delta is slot row[0]'s chunk, every 4th stripe skipped
+    js = [int(rng.integers(0, k)) for _ in range(n)]
+    dl32 = [NULL if s % 4 == 3 else off(slots[s * (k + m)]) for s in range(n)]
+    dl64 = [0 if s % 4 == 3 else twin.addr(slots[s * (k + m)]) for s in range(n)]
+    po32 = [off(slots[s * (k + m) + k + i]) for s in range(n) for i in range(m)]
+    po64 = [twin.addr(slots[s * (k + m) + k + i]) for s in range(n) for i in range(m)]
+    c.encode_update_batch32(slab.t, shift, js, dl32, po32, parity_mask=0b101)
+    c.encode_update_batch(js, dl64, po64, parity_mask=0b101)
+    torch.cuda.synchronize()
+    assert torch.equal(slab.t, twin.t)
+    # bad arguments
+    with pytest.raises(_lib.MecError):
+        c.encode_batch32(slab.t, 13, doff, poff)
+    with pytest.raises(_lib.MecError):
+        c.encode_batch32(0, shift, doff, poff)

@@ -636,3 +636,78 @@ def test_bitslice_every_output_count(m, knobs):
         st = c.stats()
         assert st["jit_failed"] == 0 and st["jit_launches"] >= 1 + int(len(pat) > 4), (k, m, st)
         c.close()
+
+
+WIDE_ARMS = {"bitsliced": {"MEC_BITSLICE": "3"}, "one_pass": {"MEC_BITSLICE": "0"},
+             "four_row": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"}}
+
+
+@pytest.mark.parametrize("arm", list(WIDE_ARMS))
+def test_wide_fixtures_vs_reference(golden, arm, knobs):
+    """every wide fixture recorded from the reference
+    itself (tests/golden/make_golden.py wide_cases: Jerasure RS / Cauchy
+    through MemEC's plugin, ISA-L RS / Cauchy through its USE_ISAL build) —
+    m > 4 encodes, decodes of 5..8 erasures of random non-codeword stripes
+    (which pin the survivor choice and the decoding matrix, not only the
+    round trip), and the ISA-L RS pattern whose survivor matrix is singular —
+    on each wide kernel: the run-time compiled bit-sliced kernel (forced for
+    every wide launch), the one-pass kernel, and 4-row launches; strided
+    in place and as a one-map device pointer batch."""
+    from memec_amd import MecError, _lib
+    for name, value in WIDE_ARMS[arm].items():
+        knobs(name, value)
+    meta, blobs = golden
+    cases = [(n, c) for n, c in sorted(meta["cases"].items()) if c.get("wide") and c["kind"] != "encode_offsets_isal"]
+    assert len(cases) >= 50
+    jit0, bytewise_launches = {}, 0
+    for name, c in cases:
+        fam, k, m, cs, kind = c["family"], c["k"], c["m"], c["chunk"], c["kind"]
+        codec = Codec(fam, k, m, cs)
+        if kind == "encode":
+            n = c["stripes"]
+            data = dev(O.fill(n * k * cs, c["seed"]).reshape(n, k, cs))
+            par = torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)
+            codec.encode(data, par)
+            assert np.array_equal(host(par).reshape(-1), blobs[name]), (arm, name)
+            par2 = torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)
+            codec.encode_batch([data[s, j].data_ptr() for s in range(n) for j in range(k)],
+                               [par2[s, i].data_ptr() for s in range(n) for i in range(m)])
+            assert np.array_equal(host(par2).reshape(-1), blobs[name]), (arm, "batch", name)
+        else:
+            buf = O.fill((k + m) * cs, c["seed"]).reshape(k + m, cs).copy()
+            buf[c["erased"]] = 0
+            present = sum(1 << i for i in range(k + m) if i not in c["erased"])
+            chunks = dev(buf).view(1, k + m, cs).clone()
+            chunks2 = chunks.clone()
+            if kind == "decode_singular_isal":
+                with pytest.raises(MecError) as ei:
+                    codec.decode(chunks, present)
+                assert ei.value.code == _lib.MEC_ESINGULAR, (arm, name)
+                res = codec.decode_batch([chunks2[0, i].data_ptr() for i in range(k + m)], [present])
+                assert res == [_lib.MEC_ESINGULAR], (arm, name, res)
+                continue
+            codec.decode(chunks, present)
+            assert codec.decode_batch([chunks2[0, i].data_ptr() for i in range(k + m)], [present]) == [0]
+            for form, t in (("strided", chunks), ("batch", chunks2)):
+                got = host(t)[0]
+                for i in range(k + m):
+                    if i not in c["erased"]:
+                        assert np.array_equal(got[i], buf[i]), (arm, form, name, "survivor", i)
+                for r, e in enumerate(sorted(c["erased"])):
+                    seg = slice(r * cs, (r + 1) * cs)
+                    if kind == "decode_random":
+                        assert np.array_equal(got[e], blobs[name][seg]), (arm, form, name, e)
+                    else:  # ISA-L: the plugin's bytes for data, its own re-encode for parity (DESIGN §8)
+                        assert np.array_equal(got[e], blobs[name + "/fixed"][seg]), (arm, form, name, e)
+                        if e < k:
+                            assert np.array_equal(got[e], blobs[name][seg]), (arm, form, name, e)
+        st = codec.stats()
+        if fam != "cauchy" and cs % 16 == 0 and (kind == "encode" or len(c["erased"]) > 4):
+            bytewise_launches += 1
+            jit0[name] = st["jit_launches"]
+        codec.close()
+    assert bytewise_launches > 30
+    if arm == "bitsliced":
+        assert all(v > 0 for v in jit0.values()), [n for n, v in jit0.items() if v == 0][:5]
+    else:
+        assert all(v == 0 for v in jit0.values()), [n for n, v in jit0.items() if v][:5]

@@ -178,7 +178,7 @@ def test_isal_plugin_encode_offsets_fixtures(golden):
     (rscoding.cc:82-89); Cauchy ignores the offsets (cauchycoding.cc:78-79)."""
     meta, blobs = golden
     cases = _encode_cases(meta, "encode_offsets_isal")
-    assert len(cases) == 8
+    assert len(cases) >= 20  # 8 with m <= 4, 12 wide (round 6)
     for name, c in cases:
         k, m, cs, idx = c["k"], c["m"], c["chunk"], c["index"]
         data = O.fill(k * cs, c["seed"])
@@ -275,3 +275,41 @@ def test_isal_fixtures_reproduce_from_reference_plugin(golden):
         assert np.array_equal(par, blobs[name]), name
         n += 1
     assert n > 20
+
+
+def test_wide_fixtures_present(golden):
+    """Round 6: the wide codes are pinned on the reference itself — encodes
+    with m > 4 for every family, decodes of 5..8 erasures of random
+    non-codeword stripes through Jerasure (RS, Cauchy) and the USE_ISAL
+    plugin (data-only and mixed patterns), ISA-L startOff/endOff encodes at
+    m > 4, and an ISA-L RS pattern whose survivor matrix is singular."""
+    meta, _ = golden
+    wide = [c for c in meta["cases"].values() if c.get("wide")]
+    fams = {(c["kind"], c["family"]) for c in wide}
+    for fam in ("rs", "cauchy", "isal_rs", "isal_cauchy"):
+        assert ("encode", fam) in fams, fam
+    for fam in ("rs", "cauchy"):
+        assert ("decode_random", fam) in fams
+    for fam in ("isal_rs", "isal_cauchy"):
+        assert ("decode_random_isal", fam) in fams
+        assert ("encode_offsets_isal", fam) in fams
+    assert max(len(c["erased"]) for c in wide if c["kind"].startswith("decode")) == 8
+    assert all(c["m"] > 4 for c in wide)
+    assert ("decode_singular_isal", "isal_rs") in fams
+
+
+def test_isal_singular_pattern_refused(golden):
+    """ISA-L's gf_gen_rs_matrix is not MDS at (12,8): the reference plugin's
+    gf_invert_matrix fails on the recorded pattern and decode() returns false
+    (rscoding.cc:166-169); the oracle refuses it too, and the same pattern
+    decodes under ISA-L Cauchy (gf_gen_cauchy1_matrix is MDS)."""
+    meta, _ = golden
+    cases = _encode_cases(meta, "decode_singular_isal")
+    assert cases
+    for name, c in cases:
+        k, m, cs = c["k"], c["m"], c["chunk"]
+        buf = O.fill((k + m) * cs, c["seed"])
+        chunks = [buf[i * cs:(i + 1) * cs].copy() for i in range(k + m)]
+        assert O.decode(c["family"], k, m, chunks, c["erased"], cs) != 0, name
+        twin = name.replace("isal_rs", "isal_cauchy")
+        assert meta["cases"][twin]["kind"] == "decode_random_isal", twin

@@ -94,6 +94,13 @@ for step in "$@"; do
                     grep -h '^{' "$OUT/zcchurn_${fam}_$bg.log" >> "$OUT/zc_churn.jsonl"
                 done
             done ;;
+        batch32)  # RS(8,2)@4 KiB strided vs pointer rows vs 32-bit slab offsets on the same chunks, interleaved (tools/wide_ab.py)
+            for rnd in 1 2; do
+                for i in ${B32_SHAPES:-32 33 36 34 35 37 18 17 38}; do
+                    run "b32_${rnd}_$i" 300 python3 tools/wide_ab.py --arms auto --shape $i --steps 30 --warmup 20
+                    grep -h '^{' "$OUT/b32_${rnd}_$i.log" >> "$OUT/batch32_ab.jsonl"
+                done
+            done ;;
         tsan)  # host-TSan build (tools/tsan_build.sh, built beforehand): concurrent callers
             export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 exitcode=0 suppressions=$PWD/tools/tsan_suppressions.txt"
             for c in rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536; do

@@ -39,7 +39,10 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("isal_rs", 12, 8, 65536, 16384, "decode"), ("rs", 8, 5, 16384, 32768, "decode"),
           ("isal_cauchy", 12, 6, 65536, 16384, "decode"), ("rs", 10, 6, 65536, 16384, "decode"),
           ("rs", 8, 2, 4096, 65536, "encode"), ("rs", 8, 2, 4096, 65536, "batch"),
-          ("rs", 8, 2, 4096, 262144, "encode"), ("rs", 8, 2, 4096, 262144, "batch")]
+          ("rs", 8, 2, 4096, 262144, "encode"), ("rs", 8, 2, 4096, 262144, "batch"),
+          # 32-bit slab offsets (mec_encode_batch32, ABI 6) over the same chunks
+          ("rs", 8, 2, 4096, 65536, "batch32"), ("rs", 8, 2, 4096, 262144, "batch32"),
+          ("rs", 10, 4, 1 << 20, 4096, "batch32"), ("rs", 16, 8, 65536, 16384, "batch32")]
 
 
 ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
@@ -83,7 +86,7 @@ def run(arms_list, steps, warmup, shapes):
         c = Codec(fam, k, m, cs)
         data = torch.empty(n, k, cs, dtype=torch.uint8, device="cuda")
         fill_random(data, 1234)
-        if op in ("encode", "batch"):
+        if op in ("encode", "batch", "batch32"):
             par = torch.empty(n, m, cs, dtype=torch.uint8, device="cuda")
             if op == "encode":
                 step = lambda: c.encode(data, par)  # noqa: E731
@@ -94,6 +97,12 @@ def run(arms_list, steps, warmup, shapes):
                 dptr = (db + (np.arange(n, dtype=np.uint64)[:, None] * k + np.arange(k, dtype=np.uint64)) * cs).ravel()
                 pptr = (pb + (np.arange(n, dtype=np.uint64)[:, None] * m + np.arange(m, dtype=np.uint64)) * cs).ravel()
                 step = lambda: c.encode_batch(dptr, pptr, mem="device")  # noqa: E731
+                if op == "batch32":  # offsets in 8-byte units from the lower of the two buffers
+                    base = min(db, pb)
+                    doff = ((dptr - np.uint64(base)) >> np.uint64(3)).astype(np.uint32)
+                    poff = ((pptr - np.uint64(base)) >> np.uint64(3)).astype(np.uint32)
+                    assert int(max(dptr.max(), pptr.max()) - base) >> 3 < 2 ** 32 - 1
+                    step = lambda: c.encode_batch32(base, 3, doff, poff)  # noqa: E731
             alg = (k + m) * cs * n
             result = lambda: par  # noqa: E731
         else:
