@@ -242,6 +242,13 @@ struct HostQueue {
     std::atomic<bool> broken{false};  // a call timed out: the queue is stopped for good
     uint64_t idle_ticks = 0, timeout_ms = 5000;
     std::atomic<bool> trace{false};   // mec_queue_trace_enable
+    // MEC_QUEUE_PUSH=<bytes>: for chunks up to that size the caller streams
+    // the job's sources through the BAR into this per-slot device area
+    // (uncached, next to the device-memory descriptor), so part 0 reads them
+    // from HBM instead of across PCIe (§4.5)
+    uint8_t *push = nullptr;
+    uint32_t push_max = 0;
+    size_t push_chunk = 0;  // bytes per source in the area (chunk rounded up to 64)
     hipStream_t stream = nullptr;
     std::mutex mu;  // launches
     std::atomic<uint64_t> launches{0};
@@ -426,7 +433,9 @@ hipError_t lane_sync(Lane *l);
 // outputs, device addresses) through the resident kernel; false = not
 // eligible, no free slot, or a timed-out job that was withdrawn (nothing
 // done: the caller takes the launch path), else rc holds the result.
-bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Mat &coef, bool accumulate, int &rc);
+// hsrc (optional): the sources' host addresses, for MEC_QUEUE_PUSH.
+bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Mat &coef, bool accumulate, int &rc,
+               const uint8_t *const *hsrc = nullptr);
 // Stop the resident kernel and free the queue; false if the grid was still
 // running at the drain cap (the queue's memory is then leaked, and so must
 // be anything its jobs can address: mec_destroy keeps the staging lanes).

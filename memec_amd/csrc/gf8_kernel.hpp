@@ -18,6 +18,7 @@
 
 #include <vector>
 
+#include "knobs.hpp"
 #include "stream_common.hpp"
 
 namespace mec {
@@ -198,6 +199,55 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
 }
 
+// Write-batched in-place decode (A/B, MEC_WBATCH=T):
+// a 256-thread block codes T consecutive 4 KiB tiles of one stripe, keeping
+// every tile's outputs in registers, and stores them only after the last
+// tile's sources are in: each output chunk then receives one T x 4 KiB
+// burst per block instead of T separate 4 KiB ones between the survivors'
+// reads.  configs[2]'s in-place decode loses 3-5 points to the split layout
+// inside the DRAM channels (§5.3); this changes the write pattern, not the
+// read one.  Instantiated for the shape it tests (K = 10, R = 4, dense).
+template <int K, int R, int S, int T>
+__global__ __launch_bounds__(kThreads) void gf8_wb_kernel(const Gf8Params<K, R> p) {
+    __shared__ uint32_t tab[R * K * 8];
+    for (int t = threadIdx.x; t < R * K; t += kThreads) {
+        const Gf8Coef c = p.coef[t / K][t % K];
+        tab[t * 8 + 0] = c.t0;
+        tab[t * 8 + 1] = c.t1;
+        tab[t * 8 + 2] = c.u0;
+        tab[t * 8 + 3] = c.u1;
+        tab[t * 8 + 4] = c.v;
+    }
+    __syncthreads();
+    const uint32_t bid = block_order(p.win);
+    uint32_t stripe, st;
+    stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, p.skew, stripe, st);  // p.tiles: groups of T tiles
+    const uint8_t *sb = p.src + int64_t(stripe) * p.sss;
+    uint8_t *db = p.dst + int64_t(stripe) * p.dss;
+    __amdgpu_buffer_rsrc_t dr[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(uint64_t(uintptr_t(db + p.dst_off[i])), p.chunk);
+    u32x4 acc[T][R];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const uint32_t off = ((st * T + t) * kThreads + threadIdx.x) * 16;  // host: units % (T x 256) == 0
+        u32x4 d[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            d[j] = buf_ld<u32x4>(chunk_rsrc(uint64_t(uintptr_t(sb + p.src_off[j])), p.chunk), off, true);
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc[t][i] = u32x4{0, 0, 0, 0};
+        gf8_apply<K, R, S>(d, acc[t], tab + opaque_zero());
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+#pragma unroll
+        for (int t = 0; t < T; ++t) buf_st(acc[t][i], dr[i], ((st * T + t) * kThreads + threadIdx.x) * 16);
+}
+// K = 10, R = 4, dense, T = 2 / 4 (gf8_r4lo.hip); false elsewhere
+template <int K, int R>
+bool launch_gf8_wb(const KernelPlan &pl, Gf8Params<K, R> p, int T, hipStream_t stream);
+
 // More than 4 outputs (m > 4: RS(16,8), ISA-L RS(12,8), decodes of > 4
 // erasures) in ONE pass over the sources: a lane loads its K source units
 // once and codes `groups` row groups of R outputs from the same registers,
@@ -349,7 +399,12 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
         p.skew = pl.skew;
         p.src = L.stab ? nullptr : L.src + int64_t(s0) * L.src_stripe_stride;
         p.dst = L.stab ? nullptr : L.dst + int64_t(s0) * L.dst_stripe_stride;
-        if (L.stab) {
+        const int64_t wb = knob(kKnobWbatch);
+        if (wb > 0 && !L.stab && !L.accumulate && pl.structure == kGf8Dense && pl.win > 1 && pl.bt == kThreads &&
+            pl.sgroup == 0 && pl.skew == 0 && pl.geo.units % (uint32_t(wb) * kThreads) == 0 &&
+            launch_gf8_wb<K, R>(pl, p, int(wb), stream)) {
+            // the write-batched A/B form took the launch
+        } else if (L.stab) {
             if (pl.structure == kGf8Vand) launch_gf8_plan<K, R, true, kGf8Vand>(pl, p, stream);
             else launch_gf8_plan<K, R, true, kGf8Dense>(pl, p, stream);
         } else if (pl.structure == kGf8Xor) {
@@ -418,6 +473,14 @@ hipError_t run_gf8_mg(const Gf8MgLaunch &L, hipStream_t stream) {
     }
     return hipSuccess;
 }
+
+// the write-batched A/B form exists for (10, 4) only (gf8_r4lo.hip)
+template <int K, int R>
+bool launch_gf8_wb(const KernelPlan &, Gf8Params<K, R>, int, hipStream_t) {
+    return false;
+}
+template <>
+bool launch_gf8_wb<10, 4>(const KernelPlan &pl, Gf8Params<10, 4> p, int T, hipStream_t stream);
 
 #define MEC_GF8_ONE(K, R) template hipError_t run_gf8<K, R>(const Gf8Launch &, hipStream_t);
 #define MEC_GF8_EXT(K, R) extern template hipError_t run_gf8<K, R>(const Gf8Launch &, hipStream_t);

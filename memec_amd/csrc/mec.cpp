@@ -377,7 +377,7 @@ int zc_single(mec_ctx *c, const std::vector<const uint8_t *> &srcs, const std::v
     }
     {
         int qrc = MEC_OK;
-        if (c->hq && queue_try(c, a.data(), srcs.size(), outs.size(), coef, accumulate, qrc)) {
+        if (c->hq && queue_try(c, a.data(), srcs.size(), outs.size(), coef, accumulate, qrc, srcs.data())) {
             if (qrc == MEC_OK) count_zc(c);
             return qrc;
         }
@@ -413,8 +413,10 @@ int lane_run(mec_ctx *c, LaneHold &h, const std::vector<int64_t> &so, const std:
         std::vector<uint64_t> a(so.size() + dof.size());
         for (size_t t = 0; t < so.size(); ++t) a[t] = base + uint64_t(so[t]);
         for (size_t r = 0; r < dof.size(); ++r) a[so.size() + r] = base + uint64_t(dof[r]);
+        std::vector<const uint8_t *> hs(so.size());
+        for (size_t t = 0; t < so.size(); ++t) hs[t] = l->host + so[t];
         int qrc = MEC_OK;
-        if (queue_try(c, a.data(), so.size(), dof.size(), coef, accumulate, qrc)) {
+        if (queue_try(c, a.data(), so.size(), dof.size(), coef, accumulate, qrc, hs.data())) {
             if (qrc != MEC_OK) h.l = nullptr;
             return qrc;
         }

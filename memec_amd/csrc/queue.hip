@@ -507,6 +507,7 @@ bool queue_stop(mec_ctx *c) {
         (void)hipFree(q->act);
         (void)hipFree(q->link);
         if (q->dslot) (void)hipFree(q->dslot);
+        if (q->push) (void)hipFree(q->push);
     }
     delete[] q->hs;
     delete q;
@@ -594,6 +595,16 @@ int queue_start(mec_ctx *c, uint32_t slots) {
             (void)hipGetLastError();  // a refused allocation leaves host-memory slots
         }
     }
+    // source push area (MEC_QUEUE_PUSH, device-memory slots only): kQMaxSrc
+    // chunks per slot
+    q->push_max = uint32_t(env_u64("MEC_QUEUE_PUSH", 0));
+    if (q->dslot && q->push_max && c->cs <= q->push_max) {
+        q->push_chunk = (size_t(c->cs) + 63) & ~size_t(63);
+        void *pa = nullptr;
+        if (hipExtMallocWithFlags(&pa, size_t(slots) * kQMaxSrc * q->push_chunk, hipDeviceMallocUncached) == hipSuccess)
+            q->push = static_cast<uint8_t *>(pa);
+        (void)hipGetLastError();  // refused: sources stay in host memory
+    }
     q->ctl_host = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(h) + sizeof(QSlot) * slots);
     q->ctl_dev = reinterpret_cast<uint32_t *>(static_cast<uint8_t *>(d) + sizeof(QSlot) * slots);
     e = hipStreamCreateWithFlags(&q->stream, hipStreamNonBlocking);
@@ -610,6 +621,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
         (void)hipFree(q->act);
         (void)hipFree(q->link);
         if (q->dslot) (void)hipFree(q->dslot);
+        if (q->push) (void)hipFree(q->push);
         delete[] q->hs;
         return hip_fail(e, "queue stream");
     }
@@ -622,6 +634,7 @@ int queue_start(mec_ctx *c, uint32_t slots) {
             (void)hipFree(q->act);
             (void)hipFree(q->link);
             if (q->dslot) (void)hipFree(q->dslot);
+            if (q->push) (void)hipFree(q->push);
             delete[] q->hs;
             return rc;
         }
@@ -630,7 +643,31 @@ int queue_start(mec_ctx *c, uint32_t slots) {
     return MEC_OK;
 }
 
-bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Mat &coef, bool accumulate, int &rc) {
+// The job's sources streamed through the BAR into the slot's device area
+// (16-byte streaming stores; the caller's chunk data may be only 8-byte
+// aligned, ChunkPool slots), descriptor entries pointed at them.  A later
+// store fence and the sequence word follow, so the GPU that sees the word
+// sees the bytes (PCIe keeps posted writes in order).
+void push_sources(HostQueue *q, uint32_t slot, QDesc &d, size_t ns, const uint8_t *const *hsrc, uint32_t cs) {
+    uint8_t *area = q->push + size_t(slot) * kQMaxSrc * q->push_chunk;
+    for (size_t j = 0; j < ns; ++j) {
+        if (!d.src[j] || !hsrc[j]) continue;
+        __m128i *to = reinterpret_cast<__m128i *>(area + j * q->push_chunk);
+        const uint8_t *from = hsrc[j];
+        const uint32_t full = cs / 16;
+        for (uint32_t u = 0; u < full; ++u)
+            _mm_stream_si128(to + u, _mm_loadu_si128(reinterpret_cast<const __m128i *>(from + size_t(u) * 16)));
+        if (cs % 16) {
+            alignas(16) uint8_t tail[16] = {};
+            std::memcpy(tail, from + size_t(full) * 16, cs % 16);
+            _mm_stream_si128(to + full, _mm_load_si128(reinterpret_cast<const __m128i *>(tail)));
+        }
+        d.src[j] = uint64_t(uintptr_t(area + j * q->push_chunk));
+    }
+}
+
+bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Mat &coef, bool accumulate, int &rc,
+               const uint8_t *const *hsrc) {
     HostQueue *q = c->hq;
     if (!q || q->broken.load(std::memory_order_relaxed) || c->cs > q->max_chunk || ns > kQMaxSrc ||
         nd > kQMaxDst || nd == 0 || (!c->byte_wise() && (c->w < 1 || c->w > 8)))
@@ -672,6 +709,7 @@ bool queue_try(mec_ctx *c, const uint64_t *addrs, size_t ns, size_t nd, const Ma
             for (size_t j = 0; j < ns; ++j) bit_block(f, coef[r * ns + j], c->w, &mk[j][r * c->w], 1);
         std::memcpy(d.mask_w, mk, sizeof(mk));
     }
+    if (q->push && hsrc && c->cs <= q->push_max) push_sources(q, i, d, ns, hsrc, c->cs);
     const uint64_t seq = q->hs[i].seqno + 1;
     q->hs[i].seqno = seq;
     const uint64_t t_post = traced ? mono_ns() : 0;

@@ -162,14 +162,16 @@ int main(int argc, char **argv) {
     }
     const double dt = now() - t0;
     const char *co = getenv("MEMEC_GPU_COALESCE");
+    const char *push = getenv("MEC_QUEUE_PUSH");
 #ifdef CODING_BENCH_REF
     const char *which = "reference";  // MemEC's own plugin, CPU
 #else
     const char *which = "coding_adapter";
 #endif
     printf("{\"bench\": \"%s\", \"scheme\": \"%s\", \"k\": %u, \"m\": %u, \"chunk\": %u, \"workers\": %d, "
-           "\"mode\": \"%s\", \"coalesce\": %s, \"registered\": %d, \"calls_per_s\": %.1f, \"data_GiBps\": %.4f}\n",
-           which, argv[1], K, M, CS, W, argv[7], co ? co : "0", registered ? 1 : 0, calls / dt,
+           "\"mode\": \"%s\", \"coalesce\": %s, \"queue_push\": %s, \"registered\": %d, \"calls_per_s\": %.1f, "
+           "\"data_GiBps\": %.4f}\n",
+           which, argv[1], K, M, CS, W, argv[7], co ? co : "0", push && *push ? push : "0", registered ? 1 : 0, calls / dt,
            bytes / dt / 1073741824.0);
     Coding::destroy(coding);
     return 0;

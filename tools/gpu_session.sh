@@ -90,7 +90,9 @@ for step in "$@"; do
         zcchurn)  # the zero-copy test's sequence on a fresh slab per iteration, beside other GPU work (tools/zc_churn.py)
             for bg in ${ZC_BG:-none all}; do
                 for fam in ${ZC_FAMS:-rs cauchy}; do
-                    run "zcchurn_${fam}_$bg" 300 python3 -u tools/zc_churn.py --fam $fam --bg $bg --iters ${ZC_ITERS:-1500}
+                    it=${ZC_ITERS:-1500}
+                    [ "$bg" = none ] || it=${ZC_ITERS_BG:-120}  # beside other GPU work a call waits for CUs
+                    run "zcchurn_${fam}_$bg" 300 python3 -u tools/zc_churn.py --fam $fam --bg $bg --iters $it
                     grep -h '^{' "$OUT/zcchurn_${fam}_$bg.log" >> "$OUT/zc_churn.jsonl"
                 done
             done ;;
@@ -100,6 +102,19 @@ for step in "$@"; do
                     run "b32_${rnd}_$i" 300 python3 tools/wide_ab.py --arms auto --shape $i --steps 30 --warmup 20
                     grep -h '^{' "$OUT/b32_${rnd}_$i.log" >> "$OUT/batch32_ab.jsonl"
                 done
+            done ;;
+        wcap)  # bit-sliced wave caps per shape: default vs forced 4 / 5 / 6 waves per CU, interleaved (tools/wide_ab.py)
+            for i in ${WCAP_SHAPES:-6 20 4}; do
+                run "wcap_$i" 400 python3 tools/wide_ab.py --arms ${WCAP_ARMS:-bs,bsw4,bsw5,bsw6,bs} --shape $i --steps 20 --warmup 20
+                grep -h '^{' "$OUT/wcap_$i.log" >> "$OUT/wcap.jsonl"
+            done ;;
+        knobab)  # interleaved bench A/B of one knob (tools/knob_ab.sh): KNOB_VAR, KNOB_VALUES, KNOB_CONFIGS, KNOB_ROUNDS
+            run "knobab_${KNOB_VAR}" 1000 env OUT="$OUT/knob_ab_${KNOB_VAR}.jsonl" bash tools/knob_ab.sh "$KNOB_VAR" \
+                "$KNOB_VALUES" "$KNOB_CONFIGS" "${KNOB_ROUNDS:-2}" ;;
+        profab)  # kernel-trace of tools/wide_ab.py shapes (PROFAB_SHAPES): per-launch kernel time vs the step's wall time
+            for i in ${PROFAB_SHAPES:-32 33 36}; do
+                run "profab_$i" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profab_$i" -o run \
+                    -- python3 tools/wide_ab.py --arms auto --shape $i --steps 30 --warmup 20
             done ;;
         tsan)  # host-TSan build (tools/tsan_build.sh, built beforehand): concurrent callers
             export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 exitcode=0 suppressions=$PWD/tools/tsan_suppressions.txt"

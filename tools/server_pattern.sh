@@ -23,8 +23,10 @@ for c in ${CFGS:-rs,4,2,4096 rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536}; do  # s
   for mode in seal delta decode; do
     for w in ${WORKERS:-1 4 16}; do
       timeout -k 10 60 oracle/_ref/coding_bench_ref $cfg $w $SECS $mode >> "$J" || exit $?
-      for reg in 0 1; do
-        MEMEC_GPU_REGISTER=$reg timeout -k 10 60 tools/coding_bench $cfg $w $SECS $mode >> "$J" || exit $?
+      for reg in ${REGS:-0 1}; do
+        for push in ${PUSHES:-0}; do  # MEC_QUEUE_PUSH arms (sources through the BAR, §4.5)
+          MEC_QUEUE_PUSH=$push MEMEC_GPU_REGISTER=$reg timeout -k 10 60 tools/coding_bench $cfg $w $SECS $mode >> "$J" || exit $?
+        done
       done
       tail -n 3 "$J"
     done

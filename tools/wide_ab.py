@@ -97,12 +97,16 @@ def run(arms_list, steps, warmup, shapes):
                 dptr = (db + (np.arange(n, dtype=np.uint64)[:, None] * k + np.arange(k, dtype=np.uint64)) * cs).ravel()
                 pptr = (pb + (np.arange(n, dtype=np.uint64)[:, None] * m + np.arange(m, dtype=np.uint64)) * cs).ravel()
                 step = lambda: c.encode_batch(dptr, pptr, mem="device")  # noqa: E731
-                if op == "batch32":  # offsets in 8-byte units from the lower of the two buffers
+                if op == "batch32":  # offsets from the lower of the two buffers, in the smallest unit that fits
                     base = min(db, pb)
-                    doff = ((dptr - np.uint64(base)) >> np.uint64(3)).astype(np.uint32)
-                    poff = ((pptr - np.uint64(base)) >> np.uint64(3)).astype(np.uint32)
-                    assert int(max(dptr.max(), pptr.max()) - base) >> 3 < 2 ** 32 - 1
-                    step = lambda: c.encode_batch32(base, 3, doff, poff)  # noqa: E731
+                    span = int(max(dptr.max(), pptr.max()) - base) + cs
+                    sh = 3
+                    while span >> sh >= 2 ** 32 - 1:
+                        sh += 1
+                    assert all(int(x - base) % (1 << sh) == 0 for x in (dptr[:64].tolist() + pptr[:64].tolist()))
+                    doff = ((dptr - np.uint64(base)) >> np.uint64(sh)).astype(np.uint32)
+                    poff = ((pptr - np.uint64(base)) >> np.uint64(sh)).astype(np.uint32)
+                    step = lambda: c.encode_batch32(base, sh, doff, poff)  # noqa: E731
             alg = (k + m) * cs * n
             result = lambda: par  # noqa: E731
         else:
