@@ -711,3 +711,66 @@ def test_wide_fixtures_vs_reference(golden, arm, knobs):
         assert all(v > 0 for v in jit0.values()), [n for n, v in jit0.items() if v == 0][:5]
     else:
         assert all(v == 0 for v in jit0.values()), [n for n, v in jit0.items() if v][:5]
+
+
+def test_wide_knob_off_turns_jit_off_everywhere(knobs):
+    """MEC_WIDE=0 forces 4-row launches on the strided and
+    zero-copy paths as on the pointer-batch path — even with the bit-sliced
+    kernels forced on (MEC_BITSLICE=3), no launch runs one; results equal."""
+    k, m, cs, n = 12, 8, 4096, 3
+    data = O.fill(n * k * cs, 515).reshape(n, k, cs)
+    want = [np.stack(O.encode("isal_rs", k, m, list(data[s]), cs)) for s in range(n)]
+    knobs("MEC_BITSLICE", "3")
+    knobs("MEC_WIDE", "0")
+    c = Codec("isal_rs", k, m, cs)
+    d = dev(data)
+    par = torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)
+    c.encode(d, par)
+    par2 = torch.zeros(n, m, cs, dtype=torch.uint8, device=DEV)
+    c.encode_batch([d[s, j].data_ptr() for s in range(n) for j in range(k)],
+                   [par2[s, i].data_ptr() for s in range(n) for i in range(m)])
+    got, got2 = host(par), host(par2)
+    for s in range(n):
+        assert np.array_equal(got[s], want[s]) and np.array_equal(got2[s], want[s]), s
+    assert c.stats()["jit_launches"] == 0
+    knobs("MEC_WIDE", None)
+    c.encode(d, par)
+    assert np.array_equal(host(par)[0], want[0])
+    assert c.stats()["jit_launches"] >= 1
+
+
+def test_jit_queue_bounded_and_destroy_cancels(knobs):
+    """in the default async mode a decode workload that
+    walks many erasure patterns queues at most MEC_JIT_MAX_QUEUED (16)
+    compiles per context, every call stays exact on the one-pass kernel
+    meanwhile, and mec_destroy cancels what is queued — it waits for the one
+    compile already running (~1 s), not for the whole queue."""
+    import itertools
+    import time
+    knobs("MEC_BITSLICE", None)
+    k, m, cs, n = 16, 8, 4096, 2
+    c = Codec("rs", k, m, cs)
+    base = O.fill(n * (k + m) * cs, 616).reshape(n, k + m, cs)
+    pats = list(itertools.islice(itertools.combinations(range(k + m), 6), 40))
+    peak = 0
+    for pat in pats[:40:4]:
+        st = dev(base)
+        st[:, list(pat)] = 0
+        c.decode(st, sum(1 << i for i in range(k + m) if i not in pat))
+        peak = max(peak, c.stats()["jit_pending"])
+        if pat is pats[0]:
+            got = host(st)
+            for s in range(n):
+                chunks = [base[s, i].copy() for i in range(k + m)]
+                for e in pat:
+                    chunks[e][:] = 0
+                assert O.decode("rs", k, m, chunks, list(pat), cs) == 0
+                assert all(np.array_equal(got[s, i], chunks[i]) for i in range(k + m))
+    for pat in pats:
+        st = dev(base)
+        c.decode(st, sum(1 << i for i in range(k + m) if i not in pat))
+        peak = max(peak, c.stats()["jit_pending"])
+    assert peak <= 16, peak
+    t0 = time.perf_counter()
+    c.close()
+    assert time.perf_counter() - t0 < 10.0

@@ -182,6 +182,8 @@ def main():
         ("host_rs1m", lambda: host_batch("rs", 10, 4, 1 << 20, 64, reps)),
         ("host_rs4k_reg", lambda: host_batch("rs", 8, 2, 4096, 16384, reps, True)),
         ("host_rs1m_reg", lambda: host_batch("rs", 10, 4, 1 << 20, 64, reps, True)),
+        ("host_crs64k", lambda: host_batch("cauchy", 12, 4, 65536, 1024, reps)),
+        ("host_crs64k_reg", lambda: host_batch("cauchy", 12, 4, 65536, 1024, reps, True)),
         ("coalesce_off", lambda: coalescer("rs", 8, 2, 4096, 16, 200, 0)),
         ("coalesce_on", lambda: coalescer("rs", 8, 2, 4096, 16, 200, 256)),
         ("coalesce_off_reg", lambda: coalescer("rs", 8, 2, 4096, 16, 200, 0, True)),

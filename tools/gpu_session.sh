@@ -53,8 +53,12 @@ for step in "$@"; do
                 run "bench_$c" 300 python bench.py --config "$c" --no-cpu-baseline --no-extra-configs --steps 10
             done ;;
         cpu256) run bench_cpu256 400 python bench.py --cpu-threads 256 --no-extra-configs --no-secondary --steps 10 ;;
-        batch) run bench_batch 600 python tools/bench_batch.py ;;
-        e2e) run bench_e2e 400 python bench.py --e2e --no-cpu-baseline --no-extra-configs --steps 5 ;;
+        batch) run bench_batch 600 python tools/bench_batch.py ${BATCH_ONLY:+--only $BATCH_ONLY} ;;
+        e2e)  # host-memory (PCIe-inclusive) dense batches, pageable and registered, per config
+            for c in ${E2E_CONFIGS:-rs_enc crs_enc rs8_small}; do
+                run "bench_e2e_$c" 400 python bench.py --config $c --e2e --no-cpu-baseline --no-extra-configs --steps 5
+                grep -h '^{' "$OUT/bench_e2e_$c.log" >> "$OUT/bench_e2e.jsonl"
+            done ;;
         prof)
             for c in ${PROF_CONFIGS:-rs_enc}; do
                 run "prof_$c" 400 rocprofv3 --kernel-trace --stats --output-format csv \
@@ -115,6 +119,11 @@ for step in "$@"; do
             for i in ${PROFAB_SHAPES:-32 33 36}; do
                 run "profab_$i" 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profab_$i" -o run \
                     -- python3 tools/wide_ab.py --arms auto --shape $i --steps 30 --warmup 20
+            done ;;
+        profcopy)  # kernel + memory-copy trace of tools/wide_ab.py shapes: the per-call table copies beside the launches
+            for i in ${PROFAB_SHAPES:-33 35 37}; do
+                run "profcopy_$i" 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
+                    -d "$OUT/profcopy_$i" -o run -- python3 tools/wide_ab.py --arms auto --shape $i --steps 30 --warmup 20
             done ;;
         tsan)  # host-TSan build (tools/tsan_build.sh, built beforehand): concurrent callers
             export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 exitcode=0 suppressions=$PWD/tools/tsan_suppressions.txt"

@@ -71,6 +71,9 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "bsx5": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "1", "MEC_WPC": "5"},
         "bsx6": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "1", "MEC_WPC": "6"},
         "bsx7": {"MEC_BITSLICE": "3", "MEC_WPC": "7"}, "bsx8": {"MEC_BITSLICE": "3", "MEC_WPC": "8"},
+        # gathered (<= 4-output) launches: wave cap per CU (MEC_GWPC; rule 16 for 128 B-aligned chunks)
+        "gw8": {"MEC_GWPC": "8"}, "gw10": {"MEC_GWPC": "10"}, "gw12": {"MEC_GWPC": "12"}, "gw16": {"MEC_GWPC": "16"},
+        "gw20": {"MEC_GWPC": "20"}, "gw24": {"MEC_GWPC": "24"}, "gw0": {"MEC_GWPC": "0"},
         # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
         "bstwin": {"MEC_BITSLICE": "3", "PROBE": "xor"}, "bsnftwin": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0", "PROBE": "xor"}}
 KNOBS = sorted({kn for a in ARMS.values() for kn in a if kn.startswith("MEC_")})
