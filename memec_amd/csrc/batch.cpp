@@ -16,6 +16,7 @@
 // batch of mixed erasures costs one host-side plan per distinct pattern
 // (the reference rebuilds matrices per call, jerasure.c:223, 958).
 #include <cstdlib>
+#include <functional>
 #include <cstring>
 #include <thread>
 
@@ -231,7 +232,8 @@ size_t build_descs(const mec_ctx *c, const MapSet &M, std::vector<uint32_t> &out
 // per call against 76.5 for the kernel, profiles/r05/vrow/prof4k/).  A slot
 // is reused only after its previous launches finished (`done`).
 int table_upload(mec_ctx *c, const std::vector<std::pair<const void *, size_t>> &parts, TableSlot *&slot,
-                 std::vector<size_t> &offs, hipStream_t st, bool mapped, uint8_t *&base) {
+                 std::vector<size_t> &offs, hipStream_t st, bool mapped, uint8_t *&base,
+                 const std::function<int(TableSlot &, uint8_t *, hipStream_t)> &after_copy = nullptr) {
     size_t total = 0;
     offs.clear();
     for (const auto &pr : parts) {
@@ -275,8 +277,20 @@ int table_upload(mec_ctx *c, const std::vector<std::pair<const void *, size_t>> 
         return MEC_OK;
     }
     HIP_TRY(hipMemcpyAsync(t.dev, t.host, total, hipMemcpyHostToDevice, cs));
+    if (after_copy) {  // device-side work on the copied tables, on the copy stream too
+        const int rc = after_copy(t, reinterpret_cast<uint8_t *>(t.dev), cs);
+        if (rc != MEC_OK) return rc;
+    }
     HIP_TRY(hipEventRecord(t.copied, cs));
-    HIP_TRY(hipStreamWaitEvent(st, t.copied, 0));
+    // MEC_TAB_WAIT=1 (A/B): while st still runs earlier launches, wait for
+    // the copy on the host — it overlaps those launches — so the next launch
+    // queues behind them with no cross-stream dependency on the device
+    if (detail::knob(detail::kKnobTabWait) == 1 && hipStreamQuery(st) == hipErrorNotReady) {
+        HIP_TRY(hipEventSynchronize(t.copied));
+    } else {
+        (void)hipGetLastError();  // a hipStreamQuery "not ready" leaves no error behind
+        HIP_TRY(hipStreamWaitEvent(st, t.copied, 0));
+    }
     base = reinterpret_cast<uint8_t *>(t.dev);
     return MEC_OK;
 }
@@ -357,13 +371,10 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
     hold.st = st;
     std::vector<size_t> offs;
     uint8_t *dev = nullptr;
-    int rc = table_upload(c, parts, hold.t, offs, st, mapped_tables, dev);
-    if (rc != MEC_OK) return rc;
-    const uint64_t *dstab = reinterpret_cast<const uint64_t *>(dev + offs[0]);
-    const uint64_t *ddtab = reinterpret_cast<const uint64_t *>(dev + offs[same ? 0 : 1]);
-    if (o32) {  // expand the offset rows into the slot's pointer table, on st after the copy
-        TableSlot &t = *hold.t;
-        const size_t ne_s = size_t(n) * sstride, ne_d = same ? 0 : size_t(n) * dstride;
+    // 32-bit offset rows: expanded into the slot's pointer table right after
+    // the copy, on the copy stream, so the coding launch waits for one event
+    const size_t ne_s = size_t(n) * sstride, ne_d = same ? 0 : size_t(n) * dstride;
+    auto expand = [&](TableSlot &t, uint8_t *d, hipStream_t cs) -> int {
         const size_t need = (ne_s + ne_d) * 8;
         if (t.xcap < need) {
             if (t.xdev) (void)hipFree(t.xdev);
@@ -372,13 +383,20 @@ int run_gather(mec_ctx *c, const MapSet &M, const void *stab, uint32_t sstride, 
             HIP_TRY(hipMalloc(reinterpret_cast<void **>(&t.xdev), std::max<size_t>(need, size_t(1) << 20)));
             t.xcap = std::max<size_t>(need, size_t(1) << 20);
         }
-        HIP_TRY(launch_expand_rows(reinterpret_cast<const uint32_t *>(dev + offs[0]), t.xdev, o32->base, o32->shift,
-                                   ne_s, st));
+        HIP_TRY(launch_expand_rows(reinterpret_cast<const uint32_t *>(d + offs[0]), t.xdev, o32->base, o32->shift, ne_s, cs));
         if (!same)
-            HIP_TRY(launch_expand_rows(reinterpret_cast<const uint32_t *>(dev + offs[1]), t.xdev + ne_s, o32->base,
-                                       o32->shift, ne_d, st));
-        dstab = t.xdev;
-        ddtab = same ? t.xdev : t.xdev + ne_s;
+            HIP_TRY(launch_expand_rows(reinterpret_cast<const uint32_t *>(d + offs[1]), t.xdev + ne_s, o32->base,
+                                       o32->shift, ne_d, cs));
+        return MEC_OK;
+    };
+    int rc = o32 ? table_upload(c, parts, hold.t, offs, st, mapped_tables, dev, expand)
+                 : table_upload(c, parts, hold.t, offs, st, mapped_tables, dev);
+    if (rc != MEC_OK) return rc;
+    const uint64_t *dstab = reinterpret_cast<const uint64_t *>(dev + offs[0]);
+    const uint64_t *ddtab = reinterpret_cast<const uint64_t *>(dev + offs[same ? 0 : 1]);
+    if (o32) {
+        dstab = hold.t->xdev;
+        ddtab = same ? hold.t->xdev : hold.t->xdev + ne_s;
     }
     auto shape_of = [&]() -> uint8_t {
         if (!device_mem) return 0;

@@ -384,7 +384,7 @@ KernelPlan plan_bm_gather(const GatherLaunch &L, uint32_t s0) {
     return p;
 }
 
-uint32_t bs_target_waves(bool in_place, bool vand, bool gather, int rows, uint32_t tiles) {
+uint32_t bs_target_waves(bool in_place, bool vand, bool gather, int k, int rows, uint32_t tiles) {
     // A strided bit-sliced wave streams 2 KiB of every one of its 13-28
     // chunks (32-56 KiB), 4 sources ahead; uncapped, the VGPR budget puts 12
     // such waves on a CU and the memory side queues them into lower
@@ -409,9 +409,20 @@ uint32_t bs_target_waves(bool in_place, bool vand, bool gather, int rows, uint32
     // RS(16,8)@4 KiB 70.9 -> 73.2, while 6-erasure decodes lose 4-5 points at
     // 6 (RS(10,6), ISA-L Cauchy(12,6)) and so does RS(4,12)@1 MiB's decode
     // of 12 (profiles/r05/vrow/ipcap_ab_box20.jsonl, vrow_cap_ab_box14.jsonl).
+    //
+    // Round 6: split dense launches by the bytes a
+    // wave keeps in flight — 2 KiB of each of the (at most 4) sources it
+    // loads ahead plus 2 KiB of each output — against kBsInflightKiB per
+    // CU: (12,6) 20 KiB and (20,8) 24 KiB keep 6 waves, (4,12) 32 KiB takes
+    // 4.  Interleaved A/B, one box (profiles/r06/wide/wcap_r06d.jsonl; % of
+    // 8 TB/s at 4 / 5 / 6 waves, default): ISA-L Cauchy(4,12)@1 MiB 78.8 /
+    // 78.7 / 75.2 (round-5 rule 74.4-74.7); Cauchy(12,6)@64 KiB 68.8 / 68.9 /
+    // 81.9; Cauchy(20,8)@4 KiB 74.0 / 73.7 / 75.5.
     if (gather) return 6;
     if (in_place) return rows >= 8 && tiles <= kBsXcdTiles ? 6 : 8;
-    return vand ? 5 : 6;
+    if (vand) return 5;
+    const uint32_t kib = 2u * uint32_t(std::min(k, 4) + rows);
+    return clampw(kBsInflightKiB / kib, 4, 6);
 }
 
 uint32_t bs_gather_tpb() {
@@ -444,7 +455,8 @@ KernelPlan plan_bs(const BsLaunch &L, uint32_t s0) {
         const uint8_t *dst = L.dst + int64_t(s0) * L.dst_stripe_stride;
         p.win = launch_windows(src, int64_t(p.ns) * L.src_stripe_stride, dst, int64_t(p.ns) * L.dst_stripe_stride);
     }
-    p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0, bs_target_waves(p.win > 1, L.vand, L.stab != nullptr, L.rows, p.geo.tiles));
+    p.lds_dynamic = occupancy_lds(kWaveBlock, kWaveBlock, 0,
+                                  bs_target_waves(p.win > 1, L.vand, L.stab != nullptr, L.k, L.rows, p.geo.tiles));
     // XCD runs: blocks are dealt round-robin over the 8 XCDs, so a stripe's
     // blocks land on all eight and each XCD's L2 fetches its pointer row.
     // Gathered launches of <= kBsXcdTiles blocks per stripe give each XCD a

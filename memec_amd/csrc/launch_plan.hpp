@@ -197,7 +197,9 @@ KernelPlan plan_bs(const BsLaunch &L, uint32_t s0);
 // Tiles per block of a gathered bit-sliced kernel built now: MEC_BS_TPB, or 1.
 uint32_t bs_gather_tpb();
 // Resident waves per CU of a bit-sliced launch (plan_bs).
-uint32_t bs_target_waves(bool in_place, bool vand, bool gather, int rows, uint32_t tiles);
+// Bytes in flight per CU the split dense bit-sliced launches are capped to.
+constexpr uint32_t kBsInflightKiB = 144;
+uint32_t bs_target_waves(bool in_place, bool vand, bool gather, int k, int rows, uint32_t tiles);
 // xor_kernel over len bytes.
 KernelPlan plan_xor(uint64_t len);
 

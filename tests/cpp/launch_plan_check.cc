@@ -185,7 +185,7 @@ static void check_bs(int k, int rows, uint64_t chunk, uint32_t n, bool in_place,
         if (!p.ok || p.ns == 0) break;
         if (p.bt != uint32_t(kWaveBlock)) bad("bit-sliced kernels are one-wave blocks", p);
         if (knob(kKnobWpc) == kKnobUnset && p.lds_dynamic == 0) bad("bit-sliced launches are capped", p);
-        if (knob(kKnobWpc) == kKnobUnset && p.lds_dynamic * bs_target_waves(p.win > 1, vand, gather, rows, p.geo.tiles) > kLdsPerCu)
+        if (knob(kKnobWpc) == kKnobUnset && p.lds_dynamic * bs_target_waves(p.win > 1, vand, gather, k, rows, p.geo.tiles) > kLdsPerCu)
             bad("bit-sliced wave cap reserves more than a CU's LDS", p);
         if (p.xcd && p.win > 1) bad("XCD runs on a windowed launch", p);
         if (knob(kKnobBsXcd) == kKnobUnset &&

@@ -125,6 +125,16 @@ for step in "$@"; do
                 run "profcopy_$i" 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \
                     -d "$OUT/profcopy_$i" -o run -- python3 tools/wide_ab.py --arms auto --shape $i --steps 30 --warmup 20
             done ;;
+        widefull)  # every byte-wise wide shape on the default arm (the rule as built), one process per shape
+            for i in ${WIDE_ALL:-$(python3 -c "import sys; sys.path.insert(0, 'tools'); import wide_ab as w; print(' '.join(str(i) for i, s in enumerate(w.SHAPES) if s[0] != 'cauchy' and s[2] > 4))")}; do
+                run "widefull_$i" 200 python3 tools/wide_ab.py --arms auto --shape $i --steps 20 --warmup 20
+                grep -h '^{' "$OUT/widefull_$i.log" >> "$OUT/widefull.jsonl"
+            done ;;
+        tabwait)  # device batches: launch waits for its table copy on the device vs on the host while the stream is busy
+            for i in ${TW_SHAPES:-33 35 36 37 17 38}; do
+                run "tabwait_$i" 300 python3 tools/wide_ab.py --arms tw0,tw1,tw0,tw1 --shape $i --steps 30 --warmup 20
+                grep -h '^{' "$OUT/tabwait_$i.log" >> "$OUT/tabwait.jsonl"
+            done ;;
         tsan)  # host-TSan build (tools/tsan_build.sh, built beforehand): concurrent callers
             export TSAN_OPTIONS="halt_on_error=0 report_signal_unsafe=0 exitcode=0 suppressions=$PWD/tools/tsan_suppressions.txt"
             for c in rs,8,2,4096 cauchy,4,2,4096 rs,10,4,65536; do

@@ -74,6 +74,8 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         # gathered (<= 4-output) launches: wave cap per CU (MEC_GWPC; rule 16 for 128 B-aligned chunks)
         "gw8": {"MEC_GWPC": "8"}, "gw10": {"MEC_GWPC": "10"}, "gw12": {"MEC_GWPC": "12"}, "gw16": {"MEC_GWPC": "16"},
         "gw20": {"MEC_GWPC": "20"}, "gw24": {"MEC_GWPC": "24"}, "gw0": {"MEC_GWPC": "0"},
+        # pointer-table copy: the launch waits on the device (tw0, rule) or on the host while its stream is busy (tw1)
+        "tw0": {"MEC_TAB_WAIT": "0"}, "tw1": {"MEC_TAB_WAIT": "1"},
         # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
         "bstwin": {"MEC_BITSLICE": "3", "PROBE": "xor"}, "bsnftwin": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0", "PROBE": "xor"}}
 KNOBS = sorted({kn for a in ARMS.values() for kn in a if kn.startswith("MEC_")})

@@ -58,7 +58,13 @@ def bg_launch(stop, errs):
 
 def bg_queue(stop, errs):
     """Another context's resident queue serving single-stripe seals on its
-    own registered slab (a resident grid polling host memory beside us)."""
+    own registered slab (a resident grid polling host memory beside us), in
+    bursts of 400 calls with 120 ms pauses: the grid then idles out between
+    bursts (MEC_QUEUE_IDLE_MS, 50 ms), which the main loop's
+    hipHostRegister / hipHostUnregister wait for — the runtime does not
+    register or unregister host memory while a kernel is resident (a queue
+    kept busy without pause held the main loop's registration for minutes,
+    profiles/r06/parity/zc_churn_r06d_queue_busy.log)."""
     k, m, cs = 8, 2, 4096
     buf = aligned((k + m) * (cs + 8))
     buf[:] = np.random.default_rng(5).integers(0, 256, buf.size, dtype=np.uint8)
@@ -69,11 +75,13 @@ def bg_queue(stop, errs):
     want = O.encode("rs", k, m, [view[j].copy() for j in range(k)], cs)
     n = 0
     while not stop.is_set():
-        view[k][:] = 0
-        got = c.encode_host([view[j] for j in range(k)])
-        if not np.array_equal(got[0], want[0]):
-            errs.append("bg queue staged encode wrong")
-        n += 1
+        for _ in range(400):
+            view[k][:] = 0
+            got = c.encode_host([view[j] for j in range(k)])
+            if not np.array_equal(got[0], want[0]):
+                errs.append("bg queue staged encode wrong")
+            n += 1
+        time.sleep(0.12)
     c.close()
     host_unregister(buf)
     return n
@@ -106,6 +114,9 @@ def main():
     slot = cs + 8
     stop, errs, counts = threading.Event(), [], {}
     kinds = ["launch", "queue", "regchurn"] if a.bg == "all" else ([] if a.bg == "none" else a.bg.split(","))
+    if "launch" in kinds:  # torch's device init before libmec's, as in the test suite
+        import torch
+        torch.cuda.set_device(0)
     fns = {"launch": bg_launch, "queue": bg_queue, "regchurn": bg_regchurn}
     threads = []
     for kd in kinds:
@@ -119,6 +130,7 @@ def main():
         threads.append(t)
     c = Codec(a.fam, k, m, cs)
     rng = np.random.default_rng(1)
+    reg_ms = []
     bad, first, addrs = [], None, set()
     t0 = time.time()
     pat = [0, 3, 10, 13]
@@ -126,7 +138,9 @@ def main():
         buf = aligned((k + m + 1) * slot)
         buf[:] = rng.integers(0, 256, buf.size, dtype=np.uint8)
         addrs.add(buf.ctypes.data)
+        t_r = time.perf_counter()
         host_register(buf)
+        reg_ms.append((time.perf_counter() - t_r) * 1e3)
         try:
             view = [buf[i * slot + 8:i * slot + 8 + cs] for i in range(k + m + 1)]
             want = O.encode(a.fam, k, m, [view[j].copy() for j in range(k)], cs)
@@ -149,7 +163,9 @@ def main():
                     bad.append(rep)
                     print(json.dumps(rep), flush=True)
         finally:
+            t_r = time.perf_counter()
             host_unregister(buf)
+            reg_ms.append((time.perf_counter() - t_r) * 1e3)
         del buf
         if it % 50 == 0:
             print("iter %d %.1fs bad %d" % (it, time.time() - t0, len(bad)), flush=True)
@@ -160,6 +176,8 @@ def main():
     c.close()
     print(json.dumps({"fam": a.fam, "cs": cs, "iters": a.iters, "bg": a.bg, "bad_calls": len(bad),
                       "distinct_slab_addrs": len(addrs), "bg_counts": counts, "bg_errors": errs[:5],
+                      "register_unregister_ms": {"median": round(float(np.median(reg_ms)), 3),
+                                                 "max": round(float(np.max(reg_ms)), 3)},
                       "zero_copy_calls": st["zero_copy_calls"], "staged_calls": st["staged_calls"],
                       "seconds": round(time.time() - t0, 1)}), flush=True)
     return 1 if bad or errs else 0
