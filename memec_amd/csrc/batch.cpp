@@ -282,10 +282,18 @@ int table_upload(mec_ctx *c, const std::vector<std::pair<const void *, size_t>> 
         if (rc != MEC_OK) return rc;
     }
     HIP_TRY(hipEventRecord(t.copied, cs));
-    // MEC_TAB_WAIT=1 (A/B): while st still runs earlier launches, wait for
-    // the copy on the host — it overlaps those launches — so the next launch
-    // queues behind them with no cross-stream dependency on the device
-    if (detail::knob(detail::kKnobTabWait) == 1 && hipStreamQuery(st) == hipErrorNotReady) {
+    // While st still runs earlier launches, wait for the copy on the host —
+    // it overlaps those launches — so this call's launch queues behind them
+    // with no cross-stream dependency: a device-side wait on the copy's
+    // event cost 10-11 us between back-to-back launches even when the copy
+    // had finished long before (rocprofv3 kernel + copy traces,
+    // profiles/r06/batch/profcopy_*), 2.5 % of an RS(8,2)@4 KiB x 65536
+    // batch; interleaved A/B (profiles/r06/batch/tabwait_r06e.jsonl): that
+    // batch 79.9-80.6 -> 80.9-81.5 % of 8 TB/s, its 32-bit offset form
+    // 79.9-80.4 -> 81.1-81.7, RS(10,4)@1 MiB unchanged.  An idle stream
+    // keeps the device-side wait (no host block for a lone call).
+    // MEC_TAB_WAIT=0 forces the device-side wait.
+    if (detail::knob(detail::kKnobTabWait) != 0 && hipStreamQuery(st) == hipErrorNotReady) {
         HIP_TRY(hipEventSynchronize(t.copied));
     } else {
         (void)hipGetLastError();  // a hipStreamQuery "not ready" leaves no error behind
