@@ -35,6 +35,7 @@ struct Gf8Params {
     uint32_t sstride, dstride, chunk, s0;
     uint32_t units, tiles, accumulate, win;
     uint32_t nstr, sgroup, srun, skew;  // stripes in this launch, stripe group and run, tile skew (stripe_tile)
+    uint32_t xcd;                       // gathered: blocks b, b + 8, ... (one XCD) take one contiguous run (plan_gf8)
     int64_t src_off[K];
     int64_t dst_off[R];
     Gf8Coef coef[R][K];
@@ -156,7 +157,11 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
         tab[t * 8 + 4] = c.v;
     }
     __syncthreads();
-    const uint32_t bid = block_order(p.win);
+    uint32_t bid = block_order(p.win);
+    if (G && p.xcd) {  // blocks are dealt round-robin over the 8 XCDs: each XCD takes one run, so a stripe's tiles share an L2
+        const uint32_t per = gridDim.x >> 3;
+        if (bid < per * 8u) bid = (bid & 7u) * per + (bid >> 3);
+    }
     uint32_t stripe, tile;
     stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, p.skew, stripe, tile);
     uint32_t u = tile * BT + threadIdx.x;
@@ -397,6 +402,7 @@ hipError_t run_gf8(const Gf8Launch &L, hipStream_t stream) {
         p.sgroup = pl.sgroup;
         p.srun = pl.srun;
         p.skew = pl.skew;
+        p.xcd = pl.xcd;
         p.src = L.stab ? nullptr : L.src + int64_t(s0) * L.src_stripe_stride;
         p.dst = L.stab ? nullptr : L.dst + int64_t(s0) * L.dst_stripe_stride;
         const int64_t wb = knob(kKnobWbatch);

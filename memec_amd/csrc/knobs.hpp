@@ -42,6 +42,7 @@ enum Knob : int {
     kKnobBsVrow,      // MEC_BS_VROW=0|1: gathered ones fetch the pointer row in one vector load (unset: rule, 1) or per entry
     kKnobWbatch,      // MEC_WBATCH=0|2|4: in-place dense RS(10,4)-shaped decodes write T tiles' outputs per block in one burst (A/B, gf8_wb_kernel)
     kKnobTabWait,     // MEC_TAB_WAIT=0|1: a device batch's launch waits for its pointer-table copy on the device (0) or, while its stream is busy, on the host (1; unset: rule, 1)
+    kKnobGxcd,        // MEC_GXCD=0|1: one-map gathered gf8 launches deal each XCD a contiguous run of blocks (unset: rule, plan_gf8)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

@@ -241,6 +241,9 @@ KernelPlan plan_gf8(const Gf8Launch &L, uint32_t s0) {
     p.structure = vand ? kGf8Vand : kGf8Dense;
     if (L.stab) {
         p.lds_dynamic = gathered_lds(p.bt, uint32_t(L.rows * L.k * 32), L.gshape);
+        // XCD runs (A/B, MEC_GXCD; default off until measured)
+        const int64_t xk = knob(kKnobGxcd);
+        p.xcd = xk == 1 ? 1u : 0u;
     } else {
         const uint8_t *src = L.src + int64_t(s0) * L.src_stripe_stride;
         const uint8_t *dst = L.dst + int64_t(s0) * L.dst_stripe_stride;

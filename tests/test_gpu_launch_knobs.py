@@ -243,3 +243,39 @@ def test_write_batched_in_place_decode(fam, wb, knobs):
             assert O.decode(fam, k, m, chunks, pat, cs) == 0
             for i in range(k + m):
                 assert np.array_equal(outs[0][s, i], chunks[i]), (fam, wb, pat, s, i)
+
+
+@pytest.mark.parametrize("cs", [4096, 1040, 65536 + 16])
+@pytest.mark.parametrize("fam", ["rs", "isal_cauchy"])
+def test_gathered_xcd_runs(fam, cs, knobs):
+    """MEC_GXCD=1 (one-map gathered gf8 launches deal each XCD a contiguous
+    run of blocks): encode and one-pattern decode batches over scattered
+    8-byte-header slots equal the oracle, tails included."""
+    knobs("MEC_GXCD", "1")
+    k, m, n = 8, 2, 37
+    slot = cs + 8
+    rng = np.random.default_rng(cs)
+    host = O.fill(n * (k + m) * slot, 71 + cs)
+    slab = torch.from_numpy(host.copy()).to("cuda")
+    perm = rng.permutation(n * (k + m))
+    addr = lambda i: slab.data_ptr() + int(i) * slot + 8  # noqa: E731
+    c = Codec(fam, k, m, cs)
+    rows = perm.reshape(n, k + m)
+    c.encode_batch([addr(x) for x in rows[:, :k].reshape(-1)], [addr(x) for x in rows[:, k:].reshape(-1)])
+    torch.cuda.synchronize()
+    got = slab.cpu().numpy()
+    view = lambda buf, i: buf[int(i) * slot + 8:int(i) * slot + 8 + cs]  # noqa: E731
+    for s in (0, n // 2, n - 1):
+        want = O.encode(fam, k, m, [view(host, x).copy() for x in rows[s, :k]], cs)
+        for i in range(m):
+            assert np.array_equal(view(got, rows[s, k + i]), want[i]), (s, i)
+    pat = [1, 8]
+    before = slab.cpu().numpy()
+    res = c.decode_batch([addr(x) for x in rows.reshape(-1)], [sum(1 << i for i in range(k + m) if i not in pat)] * n)
+    assert res == [0] * n
+    got = slab.cpu().numpy()
+    for s in (0, n - 1):
+        chunks = [view(before, x).copy() for x in rows[s]]
+        assert O.decode(fam, k, m, chunks, pat, cs) == 0
+        for i in range(k + m):
+            assert np.array_equal(view(got, rows[s, i]), chunks[i]), (s, i)

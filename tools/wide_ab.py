@@ -63,7 +63,7 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "t1w12": {"MEC_BITSLICE": "3", "MEC_WPC": "12"}, "t1w16": {"MEC_BITSLICE": "3", "MEC_WPC": "16"},
         "bsw5": {"MEC_BITSLICE": "3", "MEC_WPC": "5"}, "bsw7": {"MEC_BITSLICE": "3", "MEC_WPC": "7"},
         "bsw12": {"MEC_BITSLICE": "3", "MEC_WPC": "12"},
-        "bsnf": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0"}, "autonf": {"MEC_BITSLICE": "2", "MEC_BS_FENCE": "0"},
+        "bsnf": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0"}, "bsf1": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "1"}, "autonf": {"MEC_BITSLICE": "2", "MEC_BS_FENCE": "0"},
         "split": {"MEC_BITSLICE": "0", "MEC_WIDE": "0"},
         # gathered pointer rows: one vector load (default) / a scalar load per entry; XCD runs; row prefetch
         "bsrow": {"MEC_BITSLICE": "3", "MEC_BS_VROW": "1"}, "bssrow": {"MEC_BITSLICE": "3", "MEC_BS_VROW": "0"},
@@ -76,6 +76,9 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "gw20": {"MEC_GWPC": "20"}, "gw24": {"MEC_GWPC": "24"}, "gw0": {"MEC_GWPC": "0"},
         # pointer-table copy: the launch waits on the device (tw0, rule) or on the host while its stream is busy (tw1)
         "tw0": {"MEC_TAB_WAIT": "0"}, "tw1": {"MEC_TAB_WAIT": "1"},
+        # one-map gathered gf8 launches: XCD runs off / on, with caps
+        "gx0": {"MEC_GXCD": "0"}, "gx1": {"MEC_GXCD": "1"}, "gx1w10": {"MEC_GXCD": "1", "MEC_GWPC": "10"},
+        "gx1w12": {"MEC_GXCD": "1", "MEC_GWPC": "12"},
         # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
         "bstwin": {"MEC_BITSLICE": "3", "PROBE": "xor"}, "bsnftwin": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0", "PROBE": "xor"}}
 KNOBS = sorted({kn for a in ARMS.values() for kn in a if kn.startswith("MEC_")})
