@@ -573,6 +573,21 @@ void copy_chunks(const std::vector<Copy> &ops, size_t len) {
     for (auto &x : th) x.join();
 }
 
+void par_memcpy(void *dst, const void *src, size_t n) {
+    if (n == 0) return;
+    constexpr size_t kPiece = size_t(1) << 20;
+    if (n < (size_t(8) << 20)) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    std::vector<Copy> ops;
+    for (size_t o = 0; o + kPiece <= n; o += kPiece)
+        ops.push_back({static_cast<uint8_t *>(dst) + o, static_cast<const uint8_t *>(src) + o});
+    copy_chunks(ops, kPiece);
+    const size_t done = n / kPiece * kPiece;
+    std::memcpy(static_cast<uint8_t *>(dst) + done, static_cast<const uint8_t *>(src) + done, n - done);
+}
+
 int pipe_ready(mec_ctx *c, size_t bytes) {
     HostPipe &P = c->pipe;
     for (int b = 0; b < 2; ++b) {

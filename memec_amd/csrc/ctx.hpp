@@ -274,10 +274,13 @@ struct mec_ctx {
     std::mutex lane_mu;
     std::vector<mec::core::Lane *> lanes_free;
     std::vector<mec::core::Lane *> lanes_all;
-    // pipelined dense host batch (mec_encode_host_batch)
+    // pipelined dense host batch (mec_encode_host_batch): HBM buffers, and
+    // pinned host staging the caller's pageable bytes are copied through
     std::mutex batch_mu;
     hipStream_t bstream[2] = {nullptr, nullptr};
     uint8_t *bdev[2] = {nullptr, nullptr};
+    uint8_t *bpin[2] = {nullptr, nullptr};
+    hipEvent_t bdone[2] = {nullptr, nullptr};
     size_t bbytes = 0;
     // pointer batches (batch.cpp)
     std::mutex tab_mu;
@@ -428,6 +431,10 @@ int shard_run(mec_ctx *c, uint32_t n, const std::function<int(mec_ctx *, uint32_
 // one staged caller, but -14 % at 16 workers x RS(8,2)@4K (the pollers
 // compete for the cores the callers need) -- profiles/r01/host/sync_ab.log.
 hipError_t lane_sync(Lane *l);
+
+// batch.cpp: memcpy of n bytes split over a few threads when large
+// (MEC_COPY_THREADS).
+void par_memcpy(void *dst, const void *src, size_t n);
 
 // queue.hip.  queue_try: run one zero-copy call (addrs = ns sources then nd
 // outputs, device addresses) through the resident kernel; false = not

@@ -528,6 +528,8 @@ void mec_destroy(mec_ctx *c) {
                 (void)hipStreamDestroy(c->bstream[i]);
             }
             if (c->bdev[i]) (void)hipFree(c->bdev[i]);
+            if (c->bpin[i]) (void)hipHostFree(c->bpin[i]);
+            if (c->bdone[i]) (void)hipEventDestroy(c->bdone[i]);
         }
         jit_release(c);
         mg_release(c);
@@ -807,19 +809,29 @@ int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint
         return MEC_OK;
     }
     count_staged(c);
+    // Staged: the caller's pageable bytes are copied by the host (a few
+    // threads) into library-owned pinned buffers, DMA'd to HBM, coded there,
+    // and the parity comes back the same way; two sub-batches in flight.  No
+    // DMA ever reads or writes the caller's pageable memory (the runtime
+    // would pin it on the fly; round 6 saw such a copy fault).
     const uint32_t sub = uint32_t(std::max<size_t>(1, std::min<size_t>(n_stripes, (size_t(256) << 20) / per)));
     const size_t need = size_t(sub) * per;
     if (c->bbytes < need) {
         for (int i = 0; i < 2; ++i) {
+            if (c->bstream[i]) (void)hipStreamSynchronize(c->bstream[i]);
             if (c->bdev[i]) (void)hipFree(c->bdev[i]);
-            c->bdev[i] = nullptr;
+            if (c->bpin[i]) (void)hipHostFree(c->bpin[i]);
+            c->bdev[i] = c->bpin[i] = nullptr;
         }
         c->bbytes = 0;
-        for (int i = 0; i < 2; ++i) HIP_TRY(hipMalloc(&c->bdev[i], need));
+        for (int i = 0; i < 2; ++i) {
+            HIP_TRY(hipMalloc(&c->bdev[i], need));
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->bpin[i]), need, hipHostMallocDefault));
+        }
         c->bbytes = need;
     }
     for (int i = 0; i < 2; ++i)
-        if (!c->bstream[i]) HIP_TRY(hipStreamCreateWithFlags(&c->bstream[i], hipStreamNonBlocking));
+        if (!c->bdone[i]) HIP_TRY(hipEventCreateWithFlags(&c->bdone[i], hipEventDisableTiming | hipEventReleaseToSystem));
     std::vector<uint32_t> rows = mask_rows(c, parity_mask), cols(c->k);
     for (uint32_t j = 0; j < c->k; ++j) cols[j] = j;
     const Mat coef = encode_rows(c, rows, cols);
@@ -827,27 +839,45 @@ int mec_encode_host_batch(mec_ctx *c, const uint8_t *data, uint8_t *parity, uint
     for (uint32_t j = 0; j < c->k; ++j) so[j] = int64_t(j) * int64_t(cs);
     for (size_t r = 0; r < rows.size(); ++r) dof[r] = int64_t(rows[r]) * int64_t(cs);
     // on any failure both streams are drained before returning, so no copy
-    // queued here still writes into the caller's buffers afterwards
+    // queued here still writes into a buffer afterwards
     auto drain = [&](int rc) {
         (void)hipStreamSynchronize(c->bstream[0]);
         (void)hipStreamSynchronize(c->bstream[1]);
         return rc;
     };
-    int b = 0;
-    for (uint32_t s0 = 0; s0 < n_stripes; s0 += sub, b ^= 1) {
-        const uint32_t ns = std::min(sub, n_stripes - s0);
-        uint8_t *dd = c->bdev[b], *dp = c->bdev[b] + size_t(sub) * dbytes;
-        hipError_t e = hipMemcpyAsync(dd, data + size_t(s0) * dbytes, size_t(ns) * dbytes, hipMemcpyHostToDevice,
-                                      c->bstream[b]);
-        if (e != hipSuccess) return drain(hip_fail(e, "hipMemcpyAsync H2D"));
-        int rc = apply(c, dd, int64_t(dbytes), so, dp, int64_t(pbytes), dof, coef, ns, false, c->bstream[b]);
+    // sub-batch i uses buffers b = i & 1: data [ns][k][cs] then parity [ns][m][cs]
+    auto enqueue = [&](uint32_t s0, uint32_t ns, int b) -> int {
+        uint8_t *hp = c->bpin[b], *dd = c->bdev[b];
+        par_memcpy(hp, data + size_t(s0) * dbytes, size_t(ns) * dbytes);
+        hipError_t e = hipMemcpyAsync(dd, hp, size_t(ns) * dbytes, hipMemcpyHostToDevice, c->bstream[b]);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync H2D");
+        uint8_t *dp = dd + size_t(sub) * dbytes;
+        const int rc = apply(c, dd, int64_t(dbytes), so, dp, int64_t(pbytes), dof, coef, ns, false, c->bstream[b]);
+        if (rc != MEC_OK) return rc;
+        e = hipMemcpyAsync(hp + size_t(sub) * dbytes, dp, size_t(ns) * pbytes, hipMemcpyDeviceToHost, c->bstream[b]);
+        if (e == hipSuccess) e = hipEventRecord(c->bdone[b], c->bstream[b]);
+        return e == hipSuccess ? MEC_OK : hip_fail(e, "hipMemcpyAsync D2H");
+    };
+    auto finish = [&](uint32_t s0, uint32_t ns, int b) -> int {
+        HIP_TRY(hipEventSynchronize(c->bdone[b]));
+        par_memcpy(parity + size_t(s0) * pbytes, c->bpin[b] + size_t(sub) * dbytes, size_t(ns) * pbytes);
+        return MEC_OK;
+    };
+    std::vector<std::pair<uint32_t, uint32_t>> items;
+    for (uint32_t s0 = 0; s0 < n_stripes; s0 += sub) items.emplace_back(s0, std::min(sub, n_stripes - s0));
+    for (size_t i = 0; i < items.size(); ++i) {
+        const int b = int(i & 1);
+        if (i >= 2) {
+            const int rc = finish(items[i - 2].first, items[i - 2].second, b);
+            if (rc != MEC_OK) return drain(rc);
+        }
+        const int rc = enqueue(items[i].first, items[i].second, b);
         if (rc != MEC_OK) return drain(rc);
-        e = hipMemcpyAsync(parity + size_t(s0) * pbytes, dp, size_t(ns) * pbytes, hipMemcpyDeviceToHost,
-                           c->bstream[b]);
-        if (e != hipSuccess) return drain(hip_fail(e, "hipMemcpyAsync D2H"));
     }
-    HIP_TRY(hipStreamSynchronize(c->bstream[0]));
-    HIP_TRY(hipStreamSynchronize(c->bstream[1]));
+    for (size_t i = items.size() >= 2 ? items.size() - 2 : 0; i < items.size(); ++i) {
+        const int rc = finish(items[i].first, items[i].second, int(i & 1));
+        if (rc != MEC_OK) return drain(rc);
+    }
     return MEC_OK;
 }
 
