@@ -266,7 +266,8 @@ int mec_encode_host_batch(mec_ctx *ctx, const uint8_t *data, uint8_t *parity,
  * takes the same ptr (MEC_EINVAL if no registered range begins there).
  * Registration is meant for long-lived ranges: each call copies the range
  * list and waits for concurrent lookups to leave the one it replaces, and
- * the HIP runtime registers / unregisters only while no kernel is resident
+ * the HIP runtime appears to register / unregister only while no kernel is
+ * resident
  * (measured: up to the 50 ms idle exit of a busy host queue, longer while
  * another context keeps its queue busy) — register slabs at setup. */
 int mec_host_register(void *ptr, size_t len);

@@ -15,9 +15,14 @@
 // loads, uniform per block).  Decode plans are cached per pattern, so a
 // batch of mixed erasures costs one host-side plan per distinct pattern
 // (the reference rebuilds matrices per call, jerasure.c:223, 958).
+#include <emmintrin.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
-#include <functional>
 #include <cstring>
+#include <functional>
 #include <thread>
 
 #include "ctx.hpp"
@@ -553,24 +558,121 @@ unsigned copy_threads() {
     return unsigned(std::max<int64_t>(1, std::min<int64_t>(v, 64)));
 }
 
+// memcpy with non-temporal stores for the staged paths' big copies: what
+// they write (staging read by DMA or a kernel, outputs handed back) is not
+// read again by this thread, so the stores skip the cache and its
+// read-for-ownership.  Callers fence (_mm_sfence) before anyone else reads.
+static void nt_copy(void *dst, const void *src, size_t n) {
+    auto *d = static_cast<uint8_t *>(dst);
+    auto *s = static_cast<const uint8_t *>(src);
+    const size_t head = (0 - reinterpret_cast<uintptr_t>(d)) & 15;
+    if (n < 1024) {
+        std::memcpy(d, s, n);
+        return;
+    }
+    std::memcpy(d, s, head);
+    d += head;
+    s += head;
+    n -= head;
+    for (; n >= 64; n -= 64, d += 64, s += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i *>(s));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i *>(s + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i *>(s + 32));
+        const __m128i e = _mm_loadu_si128(reinterpret_cast<const __m128i *>(s + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i *>(d), a);
+        _mm_stream_si128(reinterpret_cast<__m128i *>(d + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i *>(d + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i *>(d + 48), e);
+    }
+    std::memcpy(d, s, n);
+}
+
+// Long-lived helper threads for the big host copies of the staged paths.
+// Spawning the helpers per copy cost about a tenth of a staged RS(10,4)
+// 1 MiB-chunk batch (73 sub-batches x 2 copies x 8 thread starts).  One job
+// at a time (bandwidth is shared anyway); the caller works too, and chunks
+// are claimed in runs so slow threads do not hold the job back.  Against
+// threads spawned per copy: staged pointer batches +4-10 %, dense batches
+// equal or +1 % (profiles/r06/host/copy_pool_ab_r06{m,n,o,p}).  The
+// pool is deliberately leaked (its threads wait on it until the process
+// ends) and rebuilt in a forked child, which inherits no threads.
+class CopyPool {
+public:
+    static CopyPool &get() {
+        static std::mutex mu;
+        static CopyPool *pool = nullptr;
+        std::lock_guard<std::mutex> lk(mu);
+        if (!pool || pool->pid_ != getpid()) pool = new CopyPool;
+        return *pool;
+    }
+
+    void run(const Copy *ops, size_t n, size_t len, unsigned helpers) {
+        std::lock_guard<std::mutex> job(job_mu_);
+        while (threads_ < helpers) {
+            std::thread(&CopyPool::worker, this, threads_).detach();
+            ++threads_;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            ops_ = ops;
+            n_ = n;
+            len_ = len;
+            next_.store(0, std::memory_order_relaxed);
+            helpers_ = helpers;
+            active_ = helpers;
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(mu_);
+        idle_cv_.wait(lk, [&] { return active_ == 0; });
+    }
+
+private:
+    // claims runs of >= 1 MiB: per-chunk claims of 4 KiB chunks scattered
+    // each thread's writes and cost 30 % (profiles/r06/host/copy_pool_ab_r06m)
+    void drain() {
+        const size_t run = std::max<size_t>(1, (size_t(1) << 20) / len_);
+        for (size_t a; (a = next_.fetch_add(run, std::memory_order_relaxed)) < n_;)
+            for (size_t i = a, b = std::min(n_, a + run); i < b; ++i) nt_copy(ops_[i].dst, ops_[i].src, len_);
+        _mm_sfence();
+    }
+    void worker(unsigned id) {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [&] { return gen_ != seen; });
+            seen = gen_;
+            if (id >= helpers_) continue;  // not asked to help with this job
+            lk.unlock();
+            drain();
+            lk.lock();
+            if (--active_ == 0) idle_cv_.notify_one();
+        }
+    }
+
+    const pid_t pid_ = getpid();
+    std::mutex job_mu_, mu_;
+    std::condition_variable cv_, idle_cv_;
+    unsigned threads_ = 0, helpers_ = 0, active_ = 0;
+    uint64_t gen_ = 0;
+    const Copy *ops_ = nullptr;
+    size_t n_ = 0, len_ = 0;
+    std::atomic<size_t> next_{0};
+};
+
 // memcpy of many equal-sized chunks, split over a few threads when large.
 void copy_chunks(const std::vector<Copy> &ops, size_t len) {
     const size_t bytes = ops.size() * len;
     unsigned nt = 1;
     if (bytes >= (size_t(8) << 20)) nt = std::min<unsigned>(copy_threads(), std::max(1u, std::thread::hardware_concurrency() / 2));
     nt = std::min<unsigned>(nt, unsigned(ops.size()));
-    auto work = [&](unsigned t) {
-        const size_t a = ops.size() * t / nt, b = ops.size() * (t + 1) / nt;
-        for (size_t i = a; i < b; ++i) std::memcpy(ops[i].dst, ops[i].src, len);
-    };
     if (nt <= 1) {
-        work(0);
+        for (const Copy &o : ops) nt_copy(o.dst, o.src, len);
+        _mm_sfence();
         return;
     }
-    std::vector<std::thread> th;
-    for (unsigned t = 1; t < nt; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto &x : th) x.join();
+    CopyPool::get().run(ops.data(), ops.size(), len, nt - 1);
 }
 
 void par_memcpy(void *dst, const void *src, size_t n) {

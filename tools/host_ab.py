@@ -26,7 +26,9 @@ from memec_amd import Codec, host_register, host_unregister  # noqa: E402
 ARMS = {"unset": {}, "wpc0": {"MEC_WPC": "0"}, "wpc8": {"MEC_WPC": "8"}, "wpc16": {"MEC_WPC": "16"},
         "wpc24": {"MEC_WPC": "24"}, "wpc32": {"MEC_WPC": "32"}, "blk64": {"MEC_BLOCK": "64"},
         "blk256": {"MEC_BLOCK": "256"}, "gw0": {"MEC_GWPC": "0"}, "gw24": {"MEC_GWPC": "24"},
-        "gw32": {"MEC_GWPC": "32"}, "gblk64": {"MEC_GBLOCK": "64"}, "gblk256": {"MEC_GBLOCK": "256"}}
+        "gw32": {"MEC_GWPC": "32"}, "gblk64": {"MEC_GBLOCK": "64"}, "gblk256": {"MEC_GBLOCK": "256"},
+        "ct4": {"MEC_COPY_THREADS": "4"}, "ct8": {"MEC_COPY_THREADS": "8"}, "ct12": {"MEC_COPY_THREADS": "12"},
+        "ct16": {"MEC_COPY_THREADS": "16"}}
 KNOBS = sorted({k for a in ARMS.values() for k in a})
 SHAPES = [("rs", 10, 4, 1 << 20, 292), ("cauchy", 12, 4, 65536, 4096), ("rs", 8, 2, 4096, 65536)]
 
@@ -42,7 +44,7 @@ def main():
     ap.add_argument("--arms", default="unset,wpc0,wpc24")
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--modes", default="registered,pageable,slots")
+    ap.add_argument("--modes", default="registered,pageable,slots,pslots")
     a = ap.parse_args()
     arms = a.arms.split(",")
     for fam, k, m, cs, n in SHAPES:
@@ -54,7 +56,7 @@ def main():
             if mode in ("registered", "slots"):
                 host_register(d)
                 host_register(p)
-            if mode == "slots":  # pointer batch over the same buffers (one map)
+            if mode in ("slots", "pslots"):  # pointer batch over the same buffers (one map); pslots unregistered
                 dptr = (d.ctypes.data + np.arange(n * k, dtype=np.uint64) * np.uint64(cs)).astype(np.uint64)
                 pptr = (p.ctypes.data + np.arange(n * m, dtype=np.uint64) * np.uint64(cs)).astype(np.uint64)
                 step = lambda: c.encode_batch(dptr, pptr, mem="host")  # noqa: E731

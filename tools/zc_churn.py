@@ -61,8 +61,8 @@ def bg_queue(stop, errs):
     own registered slab (a resident grid polling host memory beside us), in
     bursts of 400 calls with 120 ms pauses: the grid then idles out between
     bursts (MEC_QUEUE_IDLE_MS, 50 ms), which the main loop's
-    hipHostRegister / hipHostUnregister wait for — the runtime does not
-    register or unregister host memory while a kernel is resident (a queue
+    hipHostRegister / hipHostUnregister wait for — the runtime appears not
+    to register or unregister host memory while a kernel is resident (a queue
     kept busy without pause held the main loop's registration for minutes,
     profiles/r06/parity/zc_churn_r06d_queue_busy.log)."""
     k, m, cs = 8, 2, 4096
