@@ -69,6 +69,10 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "bsrow": {"MEC_BITSLICE": "3", "MEC_BS_VROW": "1"}, "bssrow": {"MEC_BITSLICE": "3", "MEC_BS_VROW": "0"},
         "bsxcd": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "1"}, "bsnx": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "0"},
         "bsx5": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "1", "MEC_WPC": "5"},
+        "bsnxw8": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "0", "MEC_WPC": "8"},
+        "bsnxw10": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "0", "MEC_WPC": "10"},
+        "bsnxw12": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "0", "MEC_WPC": "12"},
+        "bsnxw0": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "0", "MEC_WPC": "0"},
         "bsx6": {"MEC_BITSLICE": "3", "MEC_BS_XCD": "1", "MEC_WPC": "6"},
         "bsx7": {"MEC_BITSLICE": "3", "MEC_WPC": "7"}, "bsx8": {"MEC_BITSLICE": "3", "MEC_WPC": "8"},
         # gathered (<= 4-output) launches: wave cap per CU (MEC_GWPC; rule 16 for 128 B-aligned chunks)
@@ -192,12 +196,13 @@ if __name__ == "__main__":
     ap.add_argument("--rounds", type=int, default=1, help="repeat the whole shape list")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--shape", type=int, default=-1, help="index into SHAPES (default: all)")
+    ap.add_argument("--shape", default="-1", help="comma-separated indices into SHAPES (default: all)")
     ap.add_argument("--bytewise", action="store_true", help="skip the bitmatrix (Jerasure Cauchy) shapes")
     ap.add_argument("--ops", default="", help="comma-separated ops to keep (encode, decode, batch)")
     ap.add_argument("--summarise", nargs=2, metavar=("FETCH_CSV", "WRITE_CSV"))
     a = ap.parse_args()
-    shapes = SHAPES if a.shape < 0 else [SHAPES[a.shape]]
+    idx = [int(x) for x in a.shape.split(",")]
+    shapes = SHAPES if idx == [-1] else [SHAPES[i] for i in idx]
     if a.bytewise:
         shapes = [x for x in shapes if x[0] != "cauchy"]
     if a.ops:
