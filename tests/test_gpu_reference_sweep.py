@@ -149,3 +149,136 @@ def test_random_wide_shapes_bitsliced_vs_reference_plugin(fam, knobs):
         assert st["jit_failed"] == 0, (fam, k, m, cs)
         launches += st["jit_launches"]
     assert launches >= 16  # every shape's encode at least ran on the bit-sliced kernel
+
+
+# --------------------------------------------------------------------------- host memory
+
+def _aligned(nbytes, align=4096):
+    raw = np.empty(nbytes + align, np.uint8)
+    off = (-raw.ctypes.data) % align
+    return raw[off:off + nbytes]
+
+
+HOST_ARMS = ["staged", "zerocopy", "queue"]
+
+
+@pytest.mark.parametrize("arm", HOST_ARMS)
+@pytest.mark.parametrize("fam", FAMS)
+def test_random_shapes_host_paths_vs_reference_plugin(fam, arm):
+    """The server's own calls on host chunks (include/mec.h mec_*_host, the
+    host pointer batches) over a ChunkPool-like slab (slot = 8 + chunk,
+    chunk_pool.cc:22-55), for 60 random shapes per family, against the
+    plugin: `staged` (unregistered chunks through pinned staging), `zerocopy`
+    (the slab registered, mec_host_register), `queue` (registered, the
+    resident submission queue for single-stripe calls, mec_set_host_queue).
+    Single-stripe encode, in-place decode of a random non-codeword stripe
+    and delta update, then host pointer batches with a pattern per stripe."""
+    import ctypes
+    from memec_amd import host_register, host_unregister
+    from memec_amd._lib import lib
+    vp = ctypes.c_void_p
+    queued = 0
+    rng = random.Random(0xF00D + 7 * FAMS.index(fam) + HOST_ARMS.index(arm))
+    for i, (k, m, cs) in enumerate(shapes(fam, 60, 0xAB + 11 * FAMS.index(fam) + HOST_ARMS.index(arm), 2048)):
+        n, slot = 2, cs + 8
+        slab = _aligned(n * (k + m) * slot)
+        slab[:] = O.fill(slab.size, 70000 + i)
+        seed = 80000 * (1 + FAMS.index(fam)) + 10 * i + HOST_ARMS.index(arm)
+
+        def view(s, c):
+            o = (s * (k + m) + c) * slot + 8
+            return slab[o:o + cs]
+
+        def addr(s, c):
+            return slab.ctypes.data + (s * (k + m) + c) * slot + 8
+
+        if arm != "staged":
+            host_register(slab)
+        try:
+            codec = Codec(fam, k, m, cs)
+            if arm == "queue":
+                codec.set_host_queue(4)
+            h = codec._h
+            what = (arm, fam, k, m, cs)
+            # single-stripe encode straight into the slab's parity slots
+            data = np.stack([view(0, j).copy() for j in range(k)])
+            dp = (vp * k)(*[vp(addr(0, j)) for j in range(k)])
+            pp = (vp * m)(*[vp(addr(0, k + r)) for r in range(m)])
+            assert lib().mec_encode_host(h, dp, pp) == 0, what
+            want = R.encode(fam, k, m, cs, data)
+            for r in range(m):
+                same(view(0, k + r), want[r], ("encode_host",) + what + (r,))
+            # in-place decode of a random non-codeword stripe
+            for c in range(k + m):
+                view(1, c)[:] = O.fill(cs, seed + c)
+            stripe = np.stack([view(1, c).copy() for c in range(k + m)])
+            pat = sorted(rng.sample(range(k + m), rng.randint(1, m)))
+            ok, ref = R.decode(fam, k, m, cs, stripe, pat)
+            for e in pat:
+                view(1, e)[:] = 0
+            cp = (vp * (k + m))(*[vp(addr(1, c)) for c in range(k + m)])
+            present = sum(1 << c for c in range(k + m) if c not in pat)
+            rc = lib().mec_decode_host(h, cp, ctypes.c_uint64(present))
+            if not ok:
+                assert fam == "isal_rs" and rc == _lib.MEC_ESINGULAR, what + (pat, rc)
+            else:
+                assert rc == 0, what + (pat, rc)
+                for c in range(k + m):
+                    same(view(1, c), ref[c], ("decode_host",) + what + (pat, c))
+            # delta update of one column into stripe 0's parity slots
+            j = rng.randrange(k)
+            delta = _aligned(cs)
+            delta[:] = O.fill(cs, seed + 99)
+            if arm != "staged":
+                host_register(delta)
+            try:
+                before = np.stack([view(0, k + r).copy() for r in range(m)])
+                assert lib().mec_encode_update_host(h, j, vp(delta.ctypes.data), pp) == 0, what
+            finally:
+                if arm != "staged":
+                    host_unregister(delta)
+            z = np.zeros((k, cs), np.uint8)
+            z[j] = delta
+            dwant = R.encode(fam, k, m, cs, z)
+            for r in range(m):
+                same(view(0, k + r) ^ before[r], dwant[r], ("update_host",) + what + (j, r))
+            # host pointer batches: encode both stripes, then a pattern per stripe
+            for s in range(n):
+                for c in range(k + m):
+                    view(s, c)[:] = O.fill(cs, seed + 1000 * (s + 1) + c)
+            datas = [np.stack([view(s, c).copy() for c in range(k)]) for s in range(n)]
+            codec.encode_batch([addr(s, c) for s in range(n) for c in range(k)],
+                               [addr(s, k + r) for s in range(n) for r in range(m)], mem="host")
+            for s in range(n):
+                w = R.encode(fam, k, m, cs, datas[s])
+                for r in range(m):
+                    same(view(s, k + r), w[r], ("encode_batch host",) + what + (s, r))
+            stripes = [np.stack([view(s, c).copy() for c in range(k + m)]) ^ np.uint8(s + 1) for s in range(n)]
+            pats = [sorted(rng.sample(range(k + m), rng.randint(1, m))) for _ in range(n)]
+            wants = [R.decode(fam, k, m, cs, stripes[s], pats[s]) for s in range(n)]
+            for s in range(n):
+                for c in range(k + m):
+                    view(s, c)[:] = 0 if c in pats[s] else stripes[s][c]
+            res = codec.decode_batch([addr(s, c) for s in range(n) for c in range(k + m)],
+                                     [sum(1 << c for c in range(k + m) if c not in pats[s]) for s in range(n)],
+                                     mem="host")
+            for s in range(n):
+                ok, w = wants[s]
+                if not ok:
+                    assert fam == "isal_rs" and res[s] == _lib.MEC_ESINGULAR, what + (pats[s], res[s])
+                    continue
+                assert res[s] == 0, what + (pats[s], res[s])
+                for c in range(k + m):
+                    same(view(s, c), w[c], ("decode_batch host",) + what + (s, pats[s], c))
+            st = codec.stats()
+            if arm == "staged":
+                assert st["zero_copy_calls"] == 0, st
+            else:
+                assert st["staged_calls"] == 0 and st["zero_copy_calls"] + st["queue_calls"] > 0, st
+            queued += st["queue_calls"]
+            codec.close()
+        finally:
+            if arm != "staged":
+                host_unregister(slab)
+    # the queue serves single-stripe calls of <= 4 outputs; wider ones launch
+    assert (queued >= 20) if arm == "queue" else (queued == 0), queued
