@@ -156,8 +156,64 @@ static int encode_offsets(int argc, char **argv) {
     return 0;
 }
 
+// coding_test sweep <rs|cauchy> cases.txt stripes.bin out.bin
+// One case per line "k m chunk present_mask column": the next (k + m) *
+// chunk bytes of stripes.bin are one stripe (any bytes, codeword or not).
+// Per case out.bin gets: the m parities Coding::encode computes from the
+// first k chunks (index 1..m); the m parities of the server's delta form
+// (chunk `column` as the only data chunk, Coding::zeros elsewhere,
+// parity_chunk_buffer.cc:342-353); then the k + m chunks after
+// Coding::decode on the stripe with every chunk outside present_mask lost
+// (cleared first, server_peer_res_worker.cc:818-828); then one byte,
+// decode()'s return value.  tests/test_coding_adapter.py compares every
+// byte with MemEC's own plugin.
+static int sweep(int argc, char **argv) {
+    if (argc < 6) return 2;
+    CodingScheme scheme = strcmp(argv[2], "cauchy") == 0 ? CS_CAUCHY : CS_RS;
+    FILE *cf = fopen(argv[3], "r"), *sf = fopen(argv[4], "rb"), *of = fopen(argv[5], "wb");
+    if (!cf || !sf || !of) return 1;
+    unsigned k, m, cs, col;
+    unsigned long long present;
+    while (fscanf(cf, "%u %u %u %llu %u", &k, &m, &cs, &present, &col) == 5) {
+        CodingParams params;
+        params.setScheme(scheme);
+        params.setK(k);
+        params.setM(m);
+        ChunkUtil::init(cs, k);
+        Coding *coding = Coding::instantiate(scheme, params, cs);
+        if (!coding) return 1;
+        {
+            Stripe in(k, m, cs), enc(k, m, cs), dlt(k, m, cs), dec(k, m, cs);
+            for (uint32_t i = 0; i < k + m; i++)
+                if (fread(in.data(i), 1, cs, sf) != cs) return 1;
+            for (uint32_t j = 0; j < k; j++) memcpy(enc.data(j), in.data(j), cs);
+            encode_all(coding, enc);
+            std::vector<Chunk *> d(k, Coding::zeros);
+            memcpy(dlt.data(col), in.data(col), cs);
+            d[col] = dlt.c[col];
+            for (uint32_t i = 0; i < m; i++) coding->encode(&d[0], dlt.c[k + i], i + 1);
+            BitmaskArray bitmap(1, k + m);
+            for (uint32_t i = 0; i < k + m; i++) {
+                if (!(present >> i & 1)) continue;  // lost: stays cleared
+                memcpy(dec.data(i), in.data(i), cs);
+                bitmap.set(i, 0);
+            }
+            const char ok = coding->decode(&dec.c[0], &bitmap) ? 1 : 0;
+            for (uint32_t i = 0; i < m; i++) fwrite(enc.data(k + i), 1, cs, of);
+            for (uint32_t i = 0; i < m; i++) fwrite(dlt.data(k + i), 1, cs, of);
+            for (uint32_t i = 0; i < k + m; i++) fwrite(dec.data(i), 1, cs, of);
+            fwrite(&ok, 1, 1, of);
+        }
+        Coding::destroy(coding);
+    }
+    fclose(cf);
+    fclose(sf);
+    return fclose(of) == 0 ? 0 : 1;
+}
+
 int main(int argc, char **argv) {
     if (argc > 1 && strcmp(argv[1], "encode-offsets") == 0) return encode_offsets(argc, argv);
+    if (argc > 1 && strcmp(argv[1], "sweep") == 0) return sweep(argc, argv);
     if (argc < 2) {
         fprintf(stderr, "usage: %s <rs|cauchy> [k m chunk]\n", argv[0]);
         return 2;

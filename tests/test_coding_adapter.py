@@ -83,3 +83,61 @@ def test_isal_encode_offsets_match_reference(binaries, golden, tmp_path):
         r = subprocess.run(args, capture_output=True, text=True, timeout=120)
         assert r.returncode == 0, (name, r.stdout, r.stderr)
         assert np.array_equal(np.fromfile(str(out), dtype=np.uint8), blobs[name]), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fam", ["rs", "cauchy", "isal_rs", "isal_cauchy"])
+def test_adapter_random_shapes_vs_reference_plugin(binaries, fam, tmp_path):
+    """The drop-in class itself (Coding::instantiate / encode / decode, both
+    plugin builds) on 80 random shapes against MemEC's own plugin
+    (oracle/_ref, tests/_refplugin.py): encode of every parity index, the
+    server's delta form (one data chunk, Coding::zeros elsewhere) and decode
+    of a random NON-codeword stripe with 1..m lost chunks (and m + 1 for
+    every tenth case: decode() false in both) — byte for byte, decode()'s
+    return value included (ISA-L RS's singular patterns: false in both)."""
+    import random
+    import _oracle as O
+    import _refplugin as R
+    from _mismatch import same
+    if not R.available():
+        pytest.skip("oracle/_ref not built")
+    rng = random.Random(0xADA + len(fam))
+    cases, blobs = [], []
+    while len(cases) < 80:
+        n = rng.randint(2, 32)
+        m = rng.randint(1, n - 1)
+        k = n - m
+        cs = 8 * rng.randint(1, 1024)
+        if fam == "cauchy" and not 1 <= O.cauchy_getw(k, m, cs) <= 8:
+            continue
+        e = m + 1 if len(cases) % 10 == 9 else rng.randint(1, m)
+        lost = sorted(rng.sample(range(k + m), e))
+        present = sum(1 << i for i in range(k + m) if i not in lost)
+        stripe = O.fill((k + m) * cs, 0xC0DE00 + len(cases)).reshape(k + m, cs)
+        cases.append((k, m, cs, present, rng.randrange(k), lost))
+        blobs.append(stripe)
+    (tmp_path / "cases.txt").write_text("".join("%d %d %d %d %d\n" % c[:5] for c in cases))
+    np.concatenate([b.reshape(-1) for b in blobs]).tofile(str(tmp_path / "stripes.bin"))
+    b = binaries[1] if fam.startswith("isal") else binaries[0]
+    r = subprocess.run([b, "sweep", "cauchy" if fam.endswith("cauchy") else "rs", str(tmp_path / "cases.txt"),
+                        str(tmp_path / "stripes.bin"), str(tmp_path / "out.bin")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.stdout, r.stderr)
+    out = np.fromfile(str(tmp_path / "out.bin"), dtype=np.uint8)
+    pos = 0
+    for (k, m, cs, present, col, lost), stripe in zip(cases, blobs):
+        what = (fam, k, m, cs, lost)
+        enc = out[pos:pos + m * cs].reshape(m, cs)
+        dlt = out[pos + m * cs:pos + 2 * m * cs].reshape(m, cs)
+        dec = out[pos + 2 * m * cs:pos + (2 * m + k + m) * cs].reshape(k + m, cs)
+        ok = bool(out[pos + (3 * m + k) * cs])
+        pos += (3 * m + k) * cs + 1
+        same(enc, R.encode(fam, k, m, cs, stripe[:k]), ("encode",) + what)
+        z = np.zeros((k, cs), np.uint8)
+        z[col] = stripe[col]
+        same(dlt, R.encode(fam, k, m, cs, z), ("delta",) + what + (col,))
+        rok, want = R.decode(fam, k, m, cs, stripe, lost)
+        assert ok == rok, ("decode() return",) + what
+        if ok:
+            same(dec, want, ("decode",) + what)
+    assert pos == out.size
