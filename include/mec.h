@@ -418,7 +418,7 @@ int mec_set_probe(mec_ctx *ctx, int mode);
  * MEC_BLOCK, MEC_GBLOCK, MEC_GWPC, MEC_BM_VW, MEC_WPC, MEC_COPY_THREADS,
  * MEC_WIDE, MEC_MG_ROWS, MEC_BITSLICE, MEC_BS_WAVES, MEC_BS_PREFETCH,
  * MEC_BS_TPB, MEC_BS_FENCE, MEC_BS_XCD, MEC_BS_VROW,
- * MEC_TILE_SKEW, MEC_WBATCH, MEC_TAB_WAIT, MEC_GXCD from the environment once, at first use, never on a launch path; this
+ * MEC_TILE_SKEW, MEC_WBATCH, MEC_TAB_WAIT, MEC_GXCD, MEC_GU from the environment once, at first use, never on a launch path; this
  * call changes one at run time (same name and value syntax as the
  * variable; value NULL = unset, i.e. the built-in rule).  Each stored
  * value is one atomic word, so a concurrent launch sees the old or the new

@@ -164,20 +164,27 @@ class Codec:
         pp, _b = self._ptr_array(parity_ptrs)
         check(lib().mec_encode_batch(self._h, dp, pp, n, parity_mask, self._mem(mem), self._stream_for(mem, stream)))
 
-    def decode_batch(self, chunk_ptrs, present_masks, mem="device", stream=None):
-        """Returns the per-stripe status list (0 ok, MEC_ETOOMANY, ...)."""
+    @staticmethod
+    def _results(rc, res, as_array):
+        """Per-stripe statuses (numpy int32) -> list, or the array itself
+        (as_array: no per-stripe Python objects, for large batches)."""
+        if rc < 0 and not (res == rc).any():  # a failure not attributable to one stripe
+            check(rc)
+        return res if as_array else res.tolist()
+
+    def decode_batch(self, chunk_ptrs, present_masks, mem="device", stream=None, as_array=False):
+        """Returns the per-stripe status list (0 ok, MEC_ETOOMANY, ...), or
+        a numpy int32 array with as_array=True."""
         n = len(present_masks)
         if len(chunk_ptrs) != n * (self.k + self.m):
             raise ValueError("need n*(k+m) chunk pointers")
         cp, _a = self._ptr_array(chunk_ptrs)
         pmv = np.ascontiguousarray(np.asarray(present_masks, dtype=np.uint64))
         pm = ctypes.cast(pmv.ctypes.data, ctypes.POINTER(_lib.u64))
-        res = (ctypes.c_int32 * n)()
-        rc = lib().mec_decode_batch(self._h, cp, pm, n, res, self._mem(mem), self._stream_for(mem, stream))
-        out = list(res)
-        if rc < 0 and rc not in out:  # a failure not attributable to one stripe
-            check(rc)
-        return out
+        res = np.zeros(n, np.int32)
+        rc = lib().mec_decode_batch(self._h, cp, pm, n, ctypes.cast(res.ctypes.data, ctypes.POINTER(ctypes.c_int32)),
+                                    self._mem(mem), self._stream_for(mem, stream))
+        return self._results(rc, res, as_array)
 
     def encode_update_batch(self, data_index, delta_ptrs, parity_ptrs, parity_mask=0, mem="device", stream=None):
         n = len(data_index)
@@ -210,19 +217,17 @@ class Codec:
         p, _b = self._u32_array(parity_off)
         check(lib().mec_encode_batch32(self._h, self._base(base), unit_shift, d, p, n, parity_mask, _stream(stream)))
 
-    def decode_batch32(self, base, unit_shift, chunk_off, present_masks, stream=None):
+    def decode_batch32(self, base, unit_shift, chunk_off, present_masks, stream=None, as_array=False):
         n = len(present_masks)
         if len(chunk_off) != n * (self.k + self.m):
             raise ValueError("need n*(k+m) chunk offsets")
         o, _a = self._u32_array(chunk_off)
         pmv = np.ascontiguousarray(np.asarray(present_masks, dtype=np.uint64))
         pm = ctypes.cast(pmv.ctypes.data, ctypes.POINTER(_lib.u64))
-        res = (ctypes.c_int32 * n)()
-        rc = lib().mec_decode_batch32(self._h, self._base(base), unit_shift, o, pm, n, res, _stream(stream))
-        out = list(res)
-        if rc < 0 and rc not in out:
-            check(rc)
-        return out
+        res = np.zeros(n, np.int32)
+        rc = lib().mec_decode_batch32(self._h, self._base(base), unit_shift, o, pm, n,
+                                      ctypes.cast(res.ctypes.data, ctypes.POINTER(ctypes.c_int32)), _stream(stream))
+        return self._results(rc, res, as_array)
 
     def encode_update_batch32(self, base, unit_shift, data_index, delta_off, parity_off, parity_mask=0, stream=None):
         n = len(data_index)

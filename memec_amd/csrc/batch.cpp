@@ -236,6 +236,8 @@ size_t build_descs(const mec_ctx *c, const MapSet &M, std::vector<uint32_t> &out
 // 25 MB of rows, 0.45 ms of copy after each 2.1 ms launch, 63 % of 8 TB/s
 // per call against 76.5 for the kernel, profiles/r05/vrow/prof4k/).  A slot
 // is reused only after its previous launches finished (`done`).
+void table_memcpy(void *dst, const void *src, size_t n);
+
 int table_upload(mec_ctx *c, const std::vector<std::pair<const void *, size_t>> &parts, TableSlot *&slot,
                  std::vector<size_t> &offs, hipStream_t st, bool mapped, uint8_t *&base,
                  const std::function<int(TableSlot &, uint8_t *, hipStream_t)> &after_copy = nullptr) {
@@ -276,7 +278,7 @@ int table_upload(mec_ctx *c, const std::vector<std::pair<const void *, size_t>> 
     }
     uint8_t *h = reinterpret_cast<uint8_t *>(t.host);
     for (size_t i = 0; i < parts.size(); ++i)
-        if (parts[i].second) std::memcpy(h + offs[i], parts[i].first, parts[i].second);
+        if (parts[i].second) table_memcpy(h + offs[i], parts[i].first, parts[i].second);
     if (mapped) {
         base = reinterpret_cast<uint8_t *>(t.hdev);
         return MEC_OK;
@@ -675,6 +677,32 @@ void copy_chunks(const std::vector<Copy> &ops, size_t len) {
     CopyPool::get().run(ops.data(), ops.size(), len, nt - 1);
 }
 
+// A call's tables (pointer rows: 5 MB per RS(8,2)@4 KiB batch of 65536
+// stripes) into the slot's pinned staging: from 1 MiB on over a few pool
+// threads in 256 KiB pieces, so the host prepares the next call's rows well
+// inside the launch before it (one thread copying them, plus a one-map
+// decode's planning, took longer than that 0.44 ms launch: rocprofv3
+// traces, profiles/r06/batch/).
+void table_memcpy(void *dst, const void *src, size_t n) {
+    constexpr size_t kPiece = size_t(256) << 10;
+    if (n < (size_t(1) << 20)) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    const unsigned nt = std::min<unsigned>({4u, copy_threads(), std::max(1u, std::thread::hardware_concurrency() / 2)});
+    std::vector<Copy> ops;
+    for (size_t o = 0; o + kPiece <= n; o += kPiece)
+        ops.push_back({static_cast<uint8_t *>(dst) + o, static_cast<const uint8_t *>(src) + o});
+    if (nt <= 1) {
+        for (const Copy &o : ops) nt_copy(o.dst, o.src, kPiece);
+        _mm_sfence();
+    } else {
+        CopyPool::get().run(ops.data(), ops.size(), kPiece, std::min<unsigned>(nt - 1, unsigned(ops.size())));
+    }
+    const size_t done = n / kPiece * kPiece;
+    std::memcpy(static_cast<uint8_t *>(dst) + done, static_cast<const uint8_t *>(src) + done, n - done);
+}
+
 void par_memcpy(void *dst, const void *src, size_t n) {
     if (n == 0) return;
     constexpr size_t kPiece = size_t(1) << 20;
@@ -982,42 +1010,57 @@ void decode_maps(mec_ctx *c, const uint64_t *present_masks, uint32_t n_stripes, 
     M.K = c->k;
     pat.assign(n_stripes, kSkipStripe);
     std::unordered_map<uint64_t, uint16_t> ids;
-    uint64_t last_mask = ~uint64_t(0);
-    uint16_t last_id = kSkipStripe;
-    for (uint32_t s = 0; s < n_stripes; ++s) {
+    // runs of stripes with one pattern (a reconstruction batch is mostly
+    // one long run): the pattern's checks and plan once per run, per stripe
+    // only the NULL check and the two stores
+    for (uint32_t s = 0; s < n_stripes;) {
         const uint64_t present = present_masks[s] & full;
-        int src = MEC_OK;
+        uint32_t e = s + 1;
+        while (e < n_stripes && (present_masks[e] & full) == present) ++e;
         const uint32_t failed = uint32_t(__builtin_popcountll(~present & full));
         if (failed > c->m) {
-            src = fail(MEC_ETOOMANY, "Too many failure to recover (%u>%u)", failed, c->m);
-        } else if (failed > 0) {
-            for (uint32_t i = 0; i < n && src == MEC_OK; ++i)
-                if (is_null(s, i)) src = fail(MEC_EINVAL, "chunk %u pointer is NULL", i);
-            if (src == MEC_OK) {
-                if (present != last_mask) {
-                    auto it = ids.find(present);
-                    if (it == ids.end()) {
-                        const LinearPlan *plan = nullptr;
-                        src = get_plan(c, present, plan);
-                        if (src == MEC_OK) {
-                            if (M.ssel.size() >= kSkipStripe) {
-                                src = fail(MEC_EINVAL, "too many distinct erasure patterns in one batch");
-                            } else {
-                                std::vector<uint8_t> ss(plan->src.begin(), plan->src.end());
-                                std::vector<uint8_t> ds(plan->dst.begin(), plan->dst.end());
-                                it = ids.emplace(present, uint16_t(M.add(ss, ds, plan->coef))).first;
-                            }
+            for (; s < e; ++s) note(s, fail(MEC_ETOOMANY, "Too many failure to recover (%u>%u)", failed, c->m));
+            continue;
+        }
+        if (failed == 0) {
+            for (; s < e; ++s) note(s, MEC_OK);
+            continue;
+        }
+        int prc = MEC_OK;
+        uint16_t id = kSkipStripe;
+        for (; s < e; ++s) {
+            bool nul = false;
+            for (uint32_t i = 0; i < n; ++i) nul |= is_null(s, i);
+            if (nul) {
+                uint32_t i = 0;
+                while (!is_null(s, i)) ++i;
+                note(s, fail(MEC_EINVAL, "chunk %u pointer is NULL", i));
+                continue;
+            }
+            if (id == kSkipStripe && prc == MEC_OK) {  // the run's plan, at its first stripe that needs it
+                auto it = ids.find(present);
+                if (it == ids.end()) {
+                    const LinearPlan *plan = nullptr;
+                    prc = get_plan(c, present, plan);
+                    if (prc == MEC_OK) {
+                        if (M.ssel.size() >= kSkipStripe) {
+                            prc = fail(MEC_EINVAL, "too many distinct erasure patterns in one batch");
+                        } else {
+                            std::vector<uint8_t> ss(plan->src.begin(), plan->src.end());
+                            std::vector<uint8_t> ds(plan->dst.begin(), plan->dst.end());
+                            it = ids.emplace(present, uint16_t(M.add(ss, ds, plan->coef))).first;
                         }
                     }
-                    if (src == MEC_OK) {
-                        last_mask = present;
-                        last_id = it->second;
-                    }
                 }
-                if (src == MEC_OK) pat[s] = last_id;
+                if (prc == MEC_OK) id = it->second;
             }
+            if (prc != MEC_OK) {
+                note(s, prc);  // g_err still holds the plan's message
+                continue;
+            }
+            pat[s] = id;
+            note(s, MEC_OK);
         }
-        note(s, src);
     }
 }
 

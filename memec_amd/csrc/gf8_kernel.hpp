@@ -145,8 +145,15 @@ __device__ __forceinline__ void gf8_apply(const u32x4 (&d)[K], u32x4 (&acc)[R], 
 // caller's Chunk* arrays) instead of base + stripe * stride + offset; the
 // map stays in kernel arguments, so a block's only extra latency is one
 // batch of scalar loads of its pointers.
-template <int K, int R, bool G, int S, int BT>
+//
+// U = 2 (gathered one-wave blocks only, MEC_GU): a lane codes units u and
+// u + 64 of its stripe's 2 KiB tile, the wave's loads 1 KiB contiguous per
+// chunk each, one pointer-row fetch per 2 KiB; the planner uses it only
+// where every tile is whole (units % 128 == 0), so no lane is past the
+// chunk and none redoes another's unit.
+template <int K, int R, bool G, int S, int BT, int U = 1>
 __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
+    static_assert(U == 1 || (G && BT == 64 && U == 2), "two units per lane: gathered one-wave blocks");
     __shared__ uint32_t tab[R * K * 8];
     for (int t = threadIdx.x; t < R * K; t += BT) {
         const Gf8Coef c = p.coef[t / K][t % K];
@@ -164,8 +171,10 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     }
     uint32_t stripe, tile;
     stripe_tile(bid, p.tiles, p.nstr, p.sgroup, p.srun, p.skew, stripe, tile);
-    uint32_t u = tile * BT + threadIdx.x;
-    if constexpr (G) {
+    uint32_t u = tile * BT * U + threadIdx.x;
+    if constexpr (U == 2) {
+        if (u >= p.units) return;  // whole tiles: the wave is in or out
+    } else if constexpr (G) {
         if (!gather_unit<BT>(tile, p.units, u)) return;
     } else if (u >= p.units) {
         return;
@@ -189,8 +198,13 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
         else return uint64_t(uintptr_t(p.dst + int64_t(stripe) * p.dss + p.dst_off[i]));
     };
     u32x4 d[K];
+    [[maybe_unused]] u32x4 d2[U == 2 ? K : 1];
 #pragma unroll
     for (int j = 0; j < K; ++j) d[j] = buf_ld<u32x4>(chunk_rsrc(src_at(j), p.chunk), off, true);
+    if constexpr (U == 2) {
+#pragma unroll
+        for (int j = 0; j < K; ++j) d2[j] = buf_ld<u32x4>(chunk_rsrc(src_at(j), p.chunk), off + 1024u, true);
+    }
     __amdgpu_buffer_rsrc_t dr[R];
 #pragma unroll
     for (int i = 0; i < R; ++i) dr[i] = chunk_rsrc(dst_at(i), p.chunk);
@@ -202,6 +216,14 @@ __global__ __launch_bounds__(BT) void gf8_kernel(const Gf8Params<K, R> p) {
     gf8_apply<K, R, S>(d, acc, tab + opaque_zero());
 #pragma unroll
     for (int i = 0; i < R; ++i) buf_st(acc[i], dr[i], off);
+    if constexpr (U == 2) {
+        u32x4 acc2[R];
+#pragma unroll
+        for (int i = 0; i < R; ++i) acc2[i] = p.accumulate ? buf_ld<u32x4>(dr[i], off + 1024u, true) : u32x4{0, 0, 0, 0};
+        gf8_apply<K, R, S>(d2, acc2, tab + opaque_zero());
+#pragma unroll
+        for (int i = 0; i < R; ++i) buf_st(acc2[i], dr[i], off + 1024u);
+    }
 }
 
 // Write-batched in-place decode (A/B, MEC_WBATCH=T):
@@ -367,6 +389,12 @@ hipError_t launch_gf8_tail(const Gf8Launch &L, uint64_t off, hipStream_t stream)
 template <int K, int R, bool G, int S>
 void launch_gf8_plan(const KernelPlan &pl, const Gf8Params<K, R> &p, hipStream_t stream) {
     const dim3 grid(uint32_t(pl.grid)), block(pl.bt);
+    if constexpr (G) {
+        if (pl.gu == 2 && pl.bt == kWaveBlock) {
+            hipLaunchKernelGGL((gf8_kernel<K, R, G, S, kWaveBlock, 2>), grid, block, pl.lds_dynamic, stream, p);
+            return;
+        }
+    }
     if (pl.bt == kWaveBlock)
         hipLaunchKernelGGL((gf8_kernel<K, R, G, S, kWaveBlock>), grid, block, pl.lds_dynamic, stream, p);
     else

@@ -37,6 +37,7 @@ constexpr KnobSpec kSpecs[] = {
     {"MEC_WBATCH", kKnobWbatch, 0, 4, {0, 2, 4}, 3, 0},
     {"MEC_TAB_WAIT", kKnobTabWait, 0, 1, {}, 0, 0},
     {"MEC_GXCD", kKnobGxcd, 0, 1, {}, 0, 0},
+    {"MEC_GU", kKnobGu, 1, 2, {}, 0, 0},
 };
 // every knob but MEC_SGROUP's run half has its own variable
 static_assert(sizeof(kSpecs) / sizeof(kSpecs[0]) == kKnobCount - 1, "a knob whose variable is never read");

@@ -233,7 +233,12 @@ KernelPlan plan_gf8(const Gf8Launch &L, uint32_t s0) {
                   : block_threads(true, launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
                                                        int64_t(L.n_stripes) * L.dst_stripe_stride),
                                   wave_ok);
-    p.geo = geometry(L.len / 16, p.bt);
+    // one-wave one-map gathered blocks may take two units per lane (a
+    // 2 KiB tile, one pointer-row fetch per 2 KiB of every chunk) where
+    // the tiles are whole: no lane past the chunk (MEC_GU A/B)
+    const int64_t gk = L.stab && p.bt == uint32_t(kWaveBlock) ? knob(kKnobGu) : kKnobUnset;
+    p.gu = gk == 2 && (L.len / 16) % (2 * kWaveBlock) == 0 ? 2u : 1u;
+    p.geo = geometry(L.len / 16, p.bt * p.gu);
     p.ns = sub_stripes(p.geo, L.n_stripes, s0);
     p.grid = uint64_t(p.ns) * p.geo.tiles;
     p.lds_static = gf8_static_lds(L.k, L.rows);

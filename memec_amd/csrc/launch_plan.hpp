@@ -74,6 +74,7 @@ struct KernelPlan {
     uint32_t skew = 0;       // per-stripe tile rotation (identity map, in place; MEC_TILE_SKEW)
     uint32_t tpb = 1;        // tiles per block (bit-sliced kernels: geo.tiles = blocks per stripe)
     uint32_t xcd = 0;        // bit-sliced: blocks b, b + 8, ... (one XCD) take one run of the launch's blocks
+    uint32_t gu = 1;         // one-map gathered gf8, one-wave blocks: 16-byte units per lane (64 apart)
     Geometry geo{};
     uint32_t ns = 0;         // stripes in this launch
     uint64_t grid = 0;       // blocks

@@ -279,3 +279,54 @@ def test_gathered_xcd_runs(fam, cs, knobs):
         assert O.decode(fam, k, m, chunks, pat, cs) == 0
         for i in range(k + m):
             assert np.array_equal(view(got, rows[s, i]), chunks[i]), (s, i)
+
+
+@pytest.mark.parametrize("cs", [4096, 2048, 6144, 65536, 3072])
+@pytest.mark.parametrize("fam", ["rs", "isal_cauchy"])
+def test_gathered_two_units_per_lane(fam, cs, knobs):
+    """MEC_GU=2 (one-wave one-map gathered gf8 blocks code two 16-byte units
+    per lane, a 2 KiB tile per pointer-row fetch; only where the tiles are
+    whole, 3072 B falls back to one unit): encode, one-pattern decode and
+    delta-update batches over 128-byte-aligned scattered chunks (the
+    one-wave shape) equal the oracle on every stripe."""
+    knobs("MEC_GU", "2")
+    k, m, n = 8, 2, 67
+    rng = np.random.default_rng(cs + 1)
+    host = O.fill(n * (k + m) * cs, 91 + cs)
+    slab = torch.from_numpy(host.copy()).to("cuda")
+    perm = rng.permutation(n * (k + m))
+    addr = lambda i: slab.data_ptr() + int(i) * cs  # noqa: E731
+    view = lambda buf, i: buf[int(i) * cs:int(i) * cs + cs]  # noqa: E731
+    c = Codec(fam, k, m, cs)
+    rows = perm.reshape(n, k + m)
+    c.encode_batch([addr(x) for x in rows[:, :k].reshape(-1)], [addr(x) for x in rows[:, k:].reshape(-1)])
+    torch.cuda.synchronize()
+    got = slab.cpu().numpy()
+    for s in range(n):
+        want = O.encode(fam, k, m, [view(host, x).copy() for x in rows[s, :k]], cs)
+        for i in range(m):
+            assert np.array_equal(view(got, rows[s, k + i]), want[i]), (s, i)
+    pat = [0, 5]
+    before = got.copy()
+    for s in range(n):
+        for e in pat:
+            view(before, rows[s, e])[:] = 0
+    slab.copy_(torch.from_numpy(before))
+    res = c.decode_batch([addr(x) for x in rows.reshape(-1)], [sum(1 << i for i in range(k + m) if i not in pat)] * n)
+    assert res == [0] * n
+    after = slab.cpu().numpy()
+    for s in range(n):
+        for i in range(k + m):
+            assert np.array_equal(view(after, rows[s, i]), view(got, rows[s, i])), (s, i)
+    # delta update of column 3 into every stripe's parity (read-modify-write)
+    delta = torch.from_numpy(O.fill(n * cs, 17 + cs).reshape(n, cs)).to("cuda")
+    c.encode_update_batch([3] * n, [delta[s].data_ptr() for s in range(n)],
+                          [addr(x) for x in rows[:, k:].reshape(-1)])
+    upd = slab.cpu().numpy()
+    dh = delta.cpu().numpy()
+    for s in range(n):
+        d2 = [view(got, x).copy() for x in rows[s, :k]]
+        d2[3] ^= dh[s]
+        want = O.encode(fam, k, m, d2, cs)
+        for i in range(m):
+            assert np.array_equal(view(upd, rows[s, k + i]), want[i]), (s, i)

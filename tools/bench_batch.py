@@ -78,7 +78,7 @@ def decode_mixed(fam, k, m, cs, n, n_patterns, reps):
     base = stripe.data_ptr()
     ptrs = np.uint64(base) + np.arange(n * (k + m), dtype=np.uint64) * np.uint64(cs)
     masks = np.asarray(masks, dtype=np.uint64)
-    t = timed(lambda: c.decode_batch(ptrs, masks), reps)
+    t = timed(lambda: c.decode_batch(ptrs, masks, as_array=True), reps)
     alg = n * (k + m) * cs
     emit(test="decode_batch_mixed", family=fam, k=k, m=m, chunk=cs, stripes=n, patterns=n_patterns,
          ms=round(t * 1e3, 4), GBps=round(alg / t / 1e9, 1), data_GiBps=round(gib(n * k * cs) / t, 1))
@@ -175,6 +175,9 @@ def main():
         ("gather_crs64k_h8", lambda: device_gather("cauchy", 12, 4, 65536, 4096, 8, reps)),
     ]
     tests += [("decode_mixed_%d" % n, (lambda n=n: decode_mixed("rs", 10, 4, 65536, 4096, n, reps)))
+              for n in (1, 4, 14, 64)]
+    # MemEC's default chunk (bin/config: chunk=4096): reconstruction batches of 4 KiB stripes
+    tests += [("decode_mixed4k_%d" % n, (lambda n=n: decode_mixed("rs", 10, 4, 4096, 65536, n, reps)))
               for n in (1, 4, 14, 64)]
     tests += [
         ("decode_mixed_crs", lambda: decode_mixed("cauchy", 12, 4, 65536, 4096, 4, reps)),

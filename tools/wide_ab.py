@@ -42,7 +42,17 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("rs", 8, 2, 4096, 262144, "encode"), ("rs", 8, 2, 4096, 262144, "batch"),
           # 32-bit slab offsets (mec_encode_batch32, ABI 6) over the same chunks
           ("rs", 8, 2, 4096, 65536, "batch32"), ("rs", 8, 2, 4096, 262144, "batch32"),
-          ("rs", 10, 4, 1 << 20, 4096, "batch32"), ("rs", 16, 8, 65536, 16384, "batch32")]
+          ("rs", 10, 4, 1 << 20, 4096, "batch32"), ("rs", 16, 8, 65536, 16384, "batch32"),
+          # one-map gathered gf8 at 4 KiB and 64 KiB (MEC_GU A/B): strided and batch of the same chunks
+          ("rs", 10, 4, 4096, 65536, "encode"), ("rs", 10, 4, 4096, 65536, "batch"),
+          ("rs", 4, 2, 4096, 65536, "encode"), ("rs", 4, 2, 4096, 65536, "batch"),
+          ("rs", 10, 4, 65536, 16384, "encode"), ("rs", 10, 4, 65536, 16384, "batch"),
+          ("rs", 8, 2, 4096, 65536, "batchdec"),
+          # MEC_GU rule sweep: one-map 4 KiB batches by source and output count
+          ("rs", 2, 2, 4096, 131072, "batch"), ("rs", 3, 2, 4096, 131072, "batch"), ("rs", 5, 2, 4096, 65536, "batch"),
+          ("rs", 6, 2, 4096, 65536, "batch"), ("rs", 4, 1, 4096, 131072, "batch"), ("rs", 4, 3, 4096, 65536, "batch"),
+          ("rs", 4, 4, 4096, 65536, "batch"), ("rs", 4, 2, 4096, 65536, "batchdec"), ("rs", 4, 2, 8192, 32768, "batch"),
+          ("rs", 4, 2, 65536, 4096, "batch")]
 
 
 ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
@@ -83,6 +93,10 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         # one-map gathered gf8 launches: XCD runs off / on, with caps
         "gx0": {"MEC_GXCD": "0"}, "gx1": {"MEC_GXCD": "1"}, "gx1w10": {"MEC_GXCD": "1", "MEC_GWPC": "10"},
         "gx1w12": {"MEC_GXCD": "1", "MEC_GWPC": "12"},
+        # one-map gathered gf8: two 16-byte units per lane (MEC_GU=2), with caps
+        "gu1": {"MEC_GU": "1"}, "gu2": {"MEC_GU": "2"}, "gu2w8": {"MEC_GU": "2", "MEC_GWPC": "8"},
+        "gu2w10": {"MEC_GU": "2", "MEC_GWPC": "10"}, "gu2w12": {"MEC_GU": "2", "MEC_GWPC": "12"},
+        "gu2w20": {"MEC_GU": "2", "MEC_GWPC": "20"},
         # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
         "bstwin": {"MEC_BITSLICE": "3", "PROBE": "xor"}, "bsnftwin": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0", "PROBE": "xor"}}
 KNOBS = sorted({kn for a in ARMS.values() for kn in a if kn.startswith("MEC_")})
@@ -134,7 +148,7 @@ def run(arms_list, steps, warmup, shapes):
                 sb = st.data_ptr()
                 cptr = (sb + (np.arange(n, dtype=np.uint64)[:, None] * (k + m) + np.arange(k + m, dtype=np.uint64)) * cs).ravel()
                 masks = np.full(n, present, dtype=np.uint64)
-                step = lambda: c.decode_batch(cptr, masks, mem="device")  # noqa: E731
+                step = lambda: c.decode_batch(cptr, masks, mem="device", as_array=True)  # noqa: E731
             else:
                 step = lambda: c.decode(st, present)  # noqa: E731
             alg = (k + m) * cs * n
