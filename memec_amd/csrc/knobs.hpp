@@ -43,7 +43,7 @@ enum Knob : int {
     kKnobWbatch,      // MEC_WBATCH=0|2|4: in-place dense RS(10,4)-shaped decodes write T tiles' outputs per block in one burst (A/B, gf8_wb_kernel)
     kKnobTabWait,     // MEC_TAB_WAIT=0|1: a device batch's launch waits for its pointer-table copy on the device (0) or, while its stream is busy, on the host (1; unset: rule, 1)
     kKnobGxcd,        // MEC_GXCD=0|1: one-map gathered gf8 launches deal each XCD a contiguous run of blocks (unset: rule, plan_gf8)
-    kKnobGu,          // MEC_GU=1|2: 16-byte units per lane of one-wave one-map gathered gf8 launches (unset: rule, plan_gf8)
+    kKnobGu,          // MEC_GU=1|2: 16-byte units per lane of one-wave one-map gathered gf8 launches (unset: rule, plan_gf8: 2 for k + rows <= 6)
     kKnobCount
 };
 constexpr int64_t kKnobUnset = INT64_MIN;

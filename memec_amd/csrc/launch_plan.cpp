@@ -233,11 +233,18 @@ KernelPlan plan_gf8(const Gf8Launch &L, uint32_t s0) {
                   : block_threads(true, launch_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
                                                        int64_t(L.n_stripes) * L.dst_stripe_stride),
                                   wave_ok);
-    // one-wave one-map gathered blocks may take two units per lane (a
-    // 2 KiB tile, one pointer-row fetch per 2 KiB of every chunk) where
-    // the tiles are whole: no lane past the chunk (MEC_GU A/B)
-    const int64_t gk = L.stab && p.bt == uint32_t(kWaveBlock) ? knob(kKnobGu) : kKnobUnset;
-    p.gu = gk == 2 && (L.len / 16) % (2 * kWaveBlock) == 0 ? 2u : 1u;
+    // one-wave one-map gathered blocks take two units per lane (a 2 KiB
+    // tile, one pointer-row fetch per 2 KiB of every chunk) where a wave's
+    // 1 KiB per chunk is at most 6 KiB (k + rows <= 6) and the tiles are
+    // whole (no lane past the chunk).  Interleaved A/B at 4 KiB-64 KiB
+    // (tools/wide_ab.py, profiles/r06/batch/gu_ab_r06s.jsonl,
+    // gu_sweep_r06s.jsonl): RS(2,2) 66 -> 78 %, RS(3,2) 72 -> 76, RS(4,1)
+    // 76 -> 82, RS(4,2) 75-78 -> 80-82; at 7 KiB and more per wave it
+    // loses (RS(5,2), RS(4,3), RS(4,4) 0-3 points, RS(8,2) / RS(10,4)
+    // 4-15).  MEC_GU=1|2 forces it.
+    const int64_t gk = L.stab && p.bt == uint32_t(kWaveBlock) ? knob(kKnobGu) : int64_t(1);
+    const bool gu_rule = L.stab && p.bt == uint32_t(kWaveBlock) && L.k + L.rows <= 6;
+    p.gu = (gk == 2 || (gk == kKnobUnset && gu_rule)) && (L.len / 16) % (2 * kWaveBlock) == 0 ? 2u : 1u;
     p.geo = geometry(L.len / 16, p.bt * p.gu);
     p.ns = sub_stripes(p.geo, L.n_stripes, s0);
     p.grid = uint64_t(p.ns) * p.geo.tiles;
