@@ -253,6 +253,17 @@ KernelPlan plan_gf8(const Gf8Launch &L, uint32_t s0) {
     p.structure = vand ? kGf8Vand : kGf8Dense;
     if (L.stab) {
         p.lds_dynamic = gathered_lds(p.bt, uint32_t(L.rows * L.k * 32), L.gshape);
+        // block windows (the in-place layouts' block order, §4.3) for
+        // decode batches — outputs addressed through the sources' own rows —
+        // of <= 2 outputs on <= 4 KiB chunks: one-map RS(8,2)@4 KiB decode
+        // batches 74.5-76.2 -> 78.7-80.8 % of 8 TB/s at 65536 and 262144
+        // stripes; RS(4,2) and ISA-L RS(6,3) at 4 KiB within +-1 point, and
+        // more outputs or larger chunks lose (RS(10,4)@1 MiB -3)
+        // (tools/wide_ab.py, profiles/r06/batch/gwin_ab_r06s.jsonl).
+        // MEC_WINDOWS=<n> forces n.
+        const int64_t wk = knob(kKnobWindows);
+        const bool dec_rows = L.stab == L.dtab && L.sstride == L.dstride;
+        p.win = wk != kKnobUnset ? uint32_t(wk) : dec_rows && L.rows <= 2 && L.len <= 4096 ? 2u : 1u;
         // XCD runs (A/B, MEC_GXCD; default off until measured)
         const int64_t xk = knob(kKnobGxcd);
         p.xcd = xk == 1 ? 1u : 0u;

@@ -52,7 +52,16 @@ SHAPES = [("rs", 16, 8, 65536, 16384, "encode"), ("isal_rs", 12, 8, 65536, 16384
           ("rs", 2, 2, 4096, 131072, "batch"), ("rs", 3, 2, 4096, 131072, "batch"), ("rs", 5, 2, 4096, 65536, "batch"),
           ("rs", 6, 2, 4096, 65536, "batch"), ("rs", 4, 1, 4096, 131072, "batch"), ("rs", 4, 3, 4096, 65536, "batch"),
           ("rs", 4, 4, 4096, 65536, "batch"), ("rs", 4, 2, 4096, 65536, "batchdec"), ("rs", 4, 2, 8192, 32768, "batch"),
-          ("rs", 4, 2, 65536, 4096, "batch")]
+          ("rs", 4, 2, 65536, 4096, "batch"),
+          # Cauchy-RS bitmatrix batches against strided launches of the same chunks
+          ("cauchy", 12, 4, 65536, 4096, "encode"), ("cauchy", 12, 4, 65536, 4096, "batch"),
+          ("cauchy", 4, 2, 4096, 65536, "encode"), ("cauchy", 4, 2, 4096, 65536, "batch"),
+          ("cauchy", 8, 2, 4096, 65536, "encode"), ("cauchy", 8, 2, 4096, 65536, "batch"),
+          ("cauchy", 12, 4, 65536, 4096, "batchdec"), ("cauchy", 4, 2, 4096, 65536, "batchdec"),
+          # one-map gf8 decode batches (block windows A/B)
+          ("rs", 10, 4, 4096, 65536, "batchdec"), ("rs", 10, 4, 65536, 16384, "batchdec"),
+          ("rs", 10, 4, 1 << 20, 1024, "batchdec"), ("isal_rs", 6, 3, 4096, 65536, "batchdec"),
+          ("rs", 8, 2, 4096, 262144, "batchdec"), ("rs", 12, 4, 16384, 16384, "batchdec")]
 
 
 ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_BITSLICE": "0"},
@@ -97,6 +106,10 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         "gu1": {"MEC_GU": "1"}, "gu2": {"MEC_GU": "2"}, "gu2w8": {"MEC_GU": "2", "MEC_GWPC": "8"},
         "gu2w10": {"MEC_GU": "2", "MEC_GWPC": "10"}, "gu2w12": {"MEC_GU": "2", "MEC_GWPC": "12"},
         "gu2w20": {"MEC_GU": "2", "MEC_GWPC": "20"},
+        # gathered block shape (MEC_GBLOCK) with caps: bitmatrix one-map batches at 4 KiB
+        "gb64": {"MEC_GBLOCK": "64"}, "gb64w16": {"MEC_GBLOCK": "64", "MEC_GWPC": "16"},
+        "gb64w12": {"MEC_GBLOCK": "64", "MEC_GWPC": "12"}, "gb64w20": {"MEC_GBLOCK": "64", "MEC_GWPC": "20"},
+        "win1": {"MEC_WINDOWS": "1"}, "win2": {"MEC_WINDOWS": "2"}, "win4": {"MEC_WINDOWS": "4"},
         # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
         "bstwin": {"MEC_BITSLICE": "3", "PROBE": "xor"}, "bsnftwin": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0", "PROBE": "xor"}}
 KNOBS = sorted({kn for a in ARMS.values() for kn in a if kn.startswith("MEC_")})
