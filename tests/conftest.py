@@ -20,6 +20,16 @@ def pytest_collection_modifyitems(config, items):
     pass
 
 
+def pytest_collection_finish(session):
+    # GPU runs: the tests' torch copies go through pinned memory
+    # (tests/_pinned_copies.py)
+    if any(item.get_closest_marker("gpu") for item in session.items):
+        import torch
+        if torch.cuda.is_available():
+            import _pinned_copies
+            _pinned_copies.install()
+
+
 @pytest.fixture(scope="session")
 def golden():
     import _oracle
