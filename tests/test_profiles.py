@@ -48,8 +48,8 @@ def test_pmc_traffic_equals_algorithmic_bytes():
 
 
 @pytest.mark.parametrize("name,kernel_of", [
-    ("configs[1]", lambda d: (d["roofline"]["kernel_ms"], "gf8_kernel<10, 4, false, 1, 64>")),
-    ("configs[2]", lambda d: (d["decode"]["kernel_ms"], "gf8_kernel<10, 4, false, 0, 256>")),
+    ("configs[1]", lambda d: (d["roofline"]["kernel_ms"], "gf8_kernel<10, 4, false, 1, 64")),
+    ("configs[2]", lambda d: (d["decode"]["kernel_ms"], "gf8_kernel<10, 4, false, 0, 256")),
     ("configs[4] encode", lambda d: (d["other_configs"]["configs[4]"]["kernel_ms"], "bm_kernel<4, 4, false, 64, 2>")),
     ("configs[4] decode", lambda d: (d["other_configs"]["configs[4]"]["decode"]["kernel_ms"],
                                      "bm_kernel<4, 4, false, 256, 4>")),
@@ -94,7 +94,7 @@ def test_bench_live_pmc_parser_matches_the_committed_summary():
     j = json.load(open(os.path.join(ROOT, "profiles", "pmc_rs_enc.json")))
     f, name = bench.pmc_per_launch(fetch, "FETCH_SIZE")
     w, _ = bench.pmc_per_launch(write, "WRITE_SIZE")
-    assert "gf8_kernel<10, 4, false, 1, 64>" in name
+    assert "gf8_kernel<10, 4, false, 1, 64" in name
     assert f == pytest.approx(j["FETCH_SIZE_kib_per_launch"], rel=1e-12)
     assert w == pytest.approx(j["WRITE_SIZE_kib_per_launch"], rel=1e-12)
 
