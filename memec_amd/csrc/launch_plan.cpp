@@ -335,6 +335,15 @@ KernelPlan plan_bm(const BmLaunch &L, uint32_t s0) {
         const bool in_place = bm_windows(L.src, int64_t(L.n_stripes) * L.src_stripe_stride, L.dst,
                                          int64_t(L.n_stripes) * L.dst_stripe_stride, cb, R, L.k) > 1;
         if (bm_lane_bytes(L.w, R, cb, in_place) == 8) p.vw = 2;
+    } else if (p.vw == 4) {
+        // gathered: 8-byte lanes on chunks of at most 4 KiB (CRS(4,2)@4 KiB
+        // batches 73.4-73.7 -> 75.2-76.4 %, CRS(8,2) 72.6-72.9 -> 73.5-73.7,
+        // CRS(4,2) decode batches +0.5-1; CRS(12,4)@64 KiB encode batches
+        // lose 1 point with them, so larger chunks keep 16 bytes;
+        // tools/wide_ab.py, profiles/r06/batch/bm_vw_ab_r06s.jsonl).
+        // MEC_BM_VW=2|4 forces either.
+        const int64_t e = knob(kKnobBmVw);
+        if (e == 2 || (e == kKnobUnset && cb <= 4096)) p.vw = 2;
     }
     // gathered: aligned chunks keep the default shape (one-wave blocks cost
     // the bitmatrix kernel 3.5 % on aligned decode batches), unaligned ones

@@ -229,7 +229,11 @@ static void check_bm(int k, int rows, int w, uint64_t packet, uint32_t n, bool i
         if (p.rows > kMaxBmOut) bad("bitmatrix rows past 8", p);
         if (p.vw != 2 && p.vw != 4) bad("lane width", p);
         if (w > 4 && p.vw != 2) bad("w > 4 takes 8-byte lanes only", p);
-        if (gather && p.vw != uint32_t(w <= 4 ? 4 : 2)) bad("gathered bm launches use the default lane width", p);
+        if (gather) {  // gathered: 8-byte lanes for w > 4, forced, or chunks of at most 4 KiB
+            const int64_t e = knob(kKnobBmVw);
+            const uint32_t want = w > 4 || e == 2 || (e == kKnobUnset && packet * uint64_t(w) <= 4096) ? 2u : 4u;
+            if (p.vw != want) bad("gathered bm launches use the rule's lane width", p);
+        }
         covered += p.ns;
         s0 += p.ns;
     }

@@ -109,6 +109,7 @@ ARMS = {"bs": {"MEC_BITSLICE": "3"}, "auto": {"MEC_BITSLICE": "2"}, "mg": {"MEC_
         # gathered block shape (MEC_GBLOCK) with caps: bitmatrix one-map batches at 4 KiB
         "gb64": {"MEC_GBLOCK": "64"}, "gb64w16": {"MEC_GBLOCK": "64", "MEC_GWPC": "16"},
         "gb64w12": {"MEC_GBLOCK": "64", "MEC_GWPC": "12"}, "gb64w20": {"MEC_GBLOCK": "64", "MEC_GWPC": "20"},
+        "vw2": {"MEC_BM_VW": "2"}, "vw4": {"MEC_BM_VW": "4"},
         "win1": {"MEC_WINDOWS": "1"}, "win2": {"MEC_WINDOWS": "2"}, "win4": {"MEC_WINDOWS": "4"},
         # arithmetic-free twins (mec_set_probe): the same launch's loads and stores, no products
         "bstwin": {"MEC_BITSLICE": "3", "PROBE": "xor"}, "bsnftwin": {"MEC_BITSLICE": "3", "MEC_BS_FENCE": "0", "PROBE": "xor"}}
