@@ -347,8 +347,12 @@ KernelPlan plan_bm(const BmLaunch &L, uint32_t s0) {
     }
     // gathered: aligned chunks keep the default shape (one-wave blocks cost
     // the bitmatrix kernel 3.5 % on aligned decode batches), unaligned ones
-    // take the capped 4-wave shape (+1-3 %; profiles/r02/host/gather_ab_bm.log)
-    const uint8_t gshape = L.gshape == 1 ? 0 : L.gshape;
+    // take the capped 4-wave shape (+1-3 %; profiles/r02/host/gather_ab_bm.log);
+    // aligned chunks of at most 4 KiB take one-wave blocks, 16 waves per CU,
+    // as the byte-wise gathered kernels do (with 8-byte lanes: CRS(8,2)@4 KiB
+    // batches 73.2-74.0 -> 77.4 %, CRS(4,2) decode batches 68.3 -> 72.6;
+    // tools/wide_ab.py, profiles/r06/batch/bm_gb_ab_r06s.jsonl)
+    const uint8_t gshape = L.gshape == 1 && cb > 4096 ? 0 : L.gshape;
     // one-wave blocks in place: chunks of kBmWaveChunk or more, and
     // 16-32 KiB chunks with <= 2 output rows and k >= 6 (8-byte lanes, 12
     // waves per CU; CRS(6,2) / (8,2) / (12,2) in place +1-5 points,
