@@ -1038,6 +1038,8 @@ void decode_maps(mec_ctx *c, const uint64_t *present_masks, uint32_t n_stripes, 
     }
     pat.assign(n_stripes, kSkipStripe);
     std::unordered_map<uint64_t, uint16_t> ids;
+    std::pair<uint64_t, uint16_t> seen[16];
+    for (auto &e : seen) e = {~uint64_t(0), kSkipStripe};  // no present mask has every bit set
     // runs of stripes with one pattern (a reconstruction batch is mostly
     // one long run): the pattern's checks and plan once per run, per stripe
     // only the NULL check and the two stores
@@ -1067,6 +1069,15 @@ void decode_maps(mec_ctx *c, const uint64_t *present_masks, uint32_t n_stripes, 
                 continue;
             }
             if (id == kSkipStripe && prc == MEC_OK) {  // the run's plan, at its first stripe that needs it
+                // a 16-entry direct-mapped cache in front of the map: mixed
+                // batches change pattern at almost every stripe
+                const uint32_t slot = uint32_t((present * 0x9E3779B97F4A7C15ull) >> 60);
+                if (seen[slot].first == present) {
+                    id = seen[slot].second;
+                    pat[s] = id;
+                    note(s, MEC_OK);
+                    continue;
+                }
                 auto it = ids.find(present);
                 if (it == ids.end()) {
                     const LinearPlan *plan = nullptr;
@@ -1081,7 +1092,10 @@ void decode_maps(mec_ctx *c, const uint64_t *present_masks, uint32_t n_stripes, 
                         }
                     }
                 }
-                if (prc == MEC_OK) id = it->second;
+                if (prc == MEC_OK) {
+                    id = it->second;
+                    seen[slot] = {present, id};
+                }
             }
             if (prc != MEC_OK) {
                 note(s, prc);  // g_err still holds the plan's message
